@@ -1,0 +1,298 @@
+#!/usr/bin/env python3
+"""bench.py -- SRCNN training throughput on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): default SRCNN (n1=64, n2=32, f1=9, f2=1,
+f3=5), fp32, 33x33 luma patches, batch 4096 tiles per GPU.  One step = the
+reference epoch body: ConfigBasedDataPipeline::execute_batch(backprop) over
+the batch (forward L1-L3, last delta, deltas, weight/bias gradients) +
+[RCCL all-reduce of the flat gradient buffer when N > 1] +
+update_parameters (momentum SGD + weight decay, batch = global tile count)
++ zeroing of the gradient accumulators.  Every kernel is HIP (libsrcnn_hip.so
+through its C ABI); inputs are resident in HBM before the timed region.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Rank 0 prints ONE JSON line.  Data is synthetic (smooth random luma patches,
+seed 1234 + rank; weights N(0, 1e-3), biases 0).
+"""
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "cnn-super-resolution_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+import torch  # noqa: E402  (device memory / streams / torch.distributed only)
+import torch.distributed as dist  # noqa: E402
+
+PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA peak
+PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+RIDGE = PEAK_FP32_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9)
+
+DEFAULT_NET = (64, 32, 9, 1, 5)
+TILE = 33
+
+
+def layer_work(net, w, h):
+    """Algorithmic FLOPs and HBM bytes per tile of every stage:
+    each tensor written once and read once per consumer, weights ignored."""
+    n1, n2, f1, f2, f3 = net
+    w1, h1 = w - f1 + 1, h - f1 + 1
+    w2, h2 = w1 - f2 + 1, h1 - f2 + 1
+    w3, h3 = w2 - f3 + 1, h2 - f3 + 1
+    X, A1, A2, A3 = 4 * w * h, 4 * w1 * h1 * n1, 4 * w2 * h2 * n2, 4 * w3 * h3
+    T = 4 * w3 * h3  # centre crop of the ground truth that is read
+    m1 = w1 * h1 * n1 * f1 * f1
+    m2 = w2 * h2 * n2 * f2 * f2 * n1
+    m3 = w3 * h3 * f3 * f3 * n2
+    return {
+        "l1_fwd": (2 * m1, X + A1),
+        "l2_fwd": (2 * m2, A1 + A2),
+        "l3_fwd": (2 * m3, A2 + A3),
+        "last_delta": (2 * w3 * h3, A3 + T + A3),
+        "delta2": (2 * m3, A3 + A2 + A2),
+        "delta1": (2 * m2, A2 + A1 + A1),
+        "grad3": (2 * m3, A2 + A3),
+        "grad2": (2 * m2, A1 + A2),
+        "grad1": (2 * m1, X + A1),
+    }
+
+
+# kernel name (srcnn_profile_*) -> the stages it performs
+KERNEL_STAGES = {
+    # generic path
+    "conv_fwd_generic": ["l1_fwd", "l2_fwd", "l3_fwd"],
+    "last_delta": ["last_delta"],
+    "conv_delta_generic": ["delta2", "delta1"],
+    "grad_partial_generic": ["grad1", "grad2", "grad3"],
+    # gfx950 specialisations
+    "l1_fwd_mfma": ["l1_fwd"],
+    "l2_fwd_mfma": ["l2_fwd"],
+    "l3_fwd": ["l3_fwd"],
+    "l12_fwd_mfma": ["l1_fwd", "l2_fwd"],
+    "l3_delta_fused": ["l3_fwd", "last_delta", "delta2"],
+    "delta2": ["delta2"],
+    "delta1_mfma": ["delta1"],
+    "grad1_mfma": ["grad1"],
+    "grad2_mfma": ["grad2"],
+    "grad3": ["grad3"],
+    "delta1_grad12_fused": ["delta1", "grad1", "grad2"],
+}
+
+
+def roofline_of(name, launches_per_step, ms_per_step, work, tiles, pmc=None):
+    stages = KERNEL_STAGES.get(name)
+    if not stages or ms_per_step <= 0:
+        return None
+    flops = sum(work[s][0] for s in stages) * tiles / launches_per_step
+    nbytes = sum(work[s][1] for s in stages) * tiles / launches_per_step
+    dur_s = ms_per_step / launches_per_step * 1e-3
+    traffic = None
+    if pmc and name in pmc:
+        traffic = pmc[name]
+    if flops / nbytes > RIDGE:
+        ach = flops / dur_s / 1e12
+        out = {"bound": "mfma", "achieved": round(ach, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+               "frac": round(ach / PEAK_FP32_TFLOPS, 4)}
+    else:
+        ach = nbytes / dur_s / 1e9
+        out = {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+               "frac": round(ach / PEAK_HBM_GBS, 4)}
+    out.update({"traffic": traffic, "kernel": name, "avg_launch_ms": round(dur_s * 1e3, 5),
+                "algorithmic_flops_per_launch": int(flops), "algorithmic_bytes_per_launch": int(nbytes)})
+    return out
+
+
+def load_pmc():
+    """Per-launch HBM bytes from the committed rocprofv3 PMC summary
+    (profiles/pmc_*.json, written by profiles/pmc_summary.py)."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json")))
+    if not files:
+        return None
+    try:
+        with open(files[-1]) as fh:
+            data = json.load(fh)
+        return {k: v["hbm_bytes_per_launch"] for k, v in data.get("kernels", {}).items()}
+    except Exception:
+        return None
+
+
+def init_params(net, P):
+    """weights N(0, 1e-3), biases 0; identical on every rank."""
+    n1, n2, f1, f2, f3 = net
+    sizes = [f1 * f1 * n1, n1, f2 * f2 * n1 * n2, n2, f3 * f3 * n2, 1]
+    assert sum(sizes) == P
+    wrng = np.random.default_rng(1234)
+    out, o = np.zeros(P, np.float32), 0
+    for i, n in enumerate(sizes):
+        if i % 2 == 0:
+            out[o:o + n] = 1e-3 * wrng.standard_normal(n)
+        o += n
+    return out
+
+
+def synthetic_batch(rng, batch, w, h):
+    """Smooth random luma patches (uniform grid upsampled x4, clipped), input
+    mean-subtracted per patch (Main_cl.cpp:141), target = patch + N(0, 0.02)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from hip_util import make_batch
+    return make_batch(rng, batch, w, h)
+
+
+def cpu_baseline(net, tiles_min=16, budget_s=12.0):
+    """Time the CPU restatement of the reference path (oracle/, OpenMP) on a
+    bounded sample of the same workload."""
+    import srcnn_oracle as orc
+    want = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    threads = orc.set_threads(want)
+    rng = np.random.default_rng(1234)
+    batch = max(tiles_min, threads * 2)
+    X, T = synthetic_batch(rng, batch, TILE, TILE)
+    params = init_params(net, orc.param_count(*net))
+    P = params.size
+    grads = np.zeros(P, np.float32)
+    mom = np.zeros(P, np.float32)
+    lr = [1e-4, 1e-4, 1e-5]
+    orc.train_fwd_bwd(net, X[:TILE * TILE], T[:TILE * TILE], TILE, TILE, 1, params, grads)  # warm
+    done, t0 = 0, time.perf_counter()
+    while True:
+        grads, _ = orc.train_fwd_bwd(net, X, T, TILE, TILE, batch, params, grads)
+        params, grads, mom = orc.update_all(net, params, grads, mom, 0.9, 1e-3, lr, batch)
+        done += batch
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    return {"value": round(done / el, 2), "unit": "tiles/s", "cores": threads, "kind": "port",
+            "sample": "%d tiles of 33x33 (default net, fwd+bwd+update) in %.1fs with the oracle C "
+                      "restatement (oracle/srcnn_oracle.c), OpenMP over tiles" % (done, el)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=4096, help="tiles per GPU per step")
+    ap.add_argument("--path", choices=["auto", "generic"], default="auto")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+
+    import srcnn_amd as S
+    S.set_path(0 if args.path == "auto" else 1)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    stream = torch.cuda.current_stream().cuda_stream
+
+    net_t = DEFAULT_NET
+    net = S.Net(*net_t)
+    B, w, h = args.batch, TILE, TILE
+    P = S.net_param_count(net)
+    rng = np.random.default_rng(1234 + rank)
+    X, T = synthetic_batch(rng, B, w, h)
+    prm = init_params(net_t, P)
+    Xd = torch.from_numpy(X).to(dev)
+    Td = torch.from_numpy(T).to(dev)
+    params = torch.from_numpy(prm).to(dev)
+    grads = torch.zeros(P, dtype=torch.float32, device=dev)
+    mom = torch.zeros(P, dtype=torch.float32, device=dev)
+    ws_bytes = S.train_workspace_bytes(net, w, h, B)
+    ws = torch.empty(ws_bytes // 4 + 64, dtype=torch.float32, device=dev)
+    lr = [1e-4, 1e-4, 1e-5]
+    global_tiles = B * world
+
+    def step():
+        S.train_fwd_bwd(net, Xd, Td, w, h, B, params, grads, None, ws, ws_bytes, stream)
+        if world > 1:
+            dist.all_reduce(grads)
+        S.update_all(net, params, grads, mom, 0.9, 1e-3, lr, global_tiles, stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    S.profile_reset()
+    S.profile_enable(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    S.profile_enable(False)
+    elapsed = t1 - t0
+    if world > 1:
+        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    stats = S.profile_stats()
+    assert np.isfinite(params.cpu().numpy()).all(), "non-finite parameters after training"
+
+    if rank == 0:
+        K = args.steps
+        value = global_tiles * K / elapsed
+        work = layer_work(net_t, w, h)
+        pmc = load_pmc()
+        kernels = {}
+        for name, (cnt, ms) in stats.items():
+            kernels[name] = {"launches_per_step": cnt / K, "ms_per_step": round(ms / K, 4)}
+        dominant = max(stats.items(), key=lambda kv: kv[1][1])[0] if stats else None
+        roof = None
+        if dominant:
+            cnt, ms = stats[dominant]
+            roof = roofline_of(dominant, cnt / K, ms / K, work, B, pmc)
+        # whole-step roofline: T_roof = sum_stage max(F/peak, B/peak)
+        t_roof = sum(max(f / (PEAK_FP32_TFLOPS * 1e12), b / (PEAK_HBM_GBS * 1e9))
+                     for f, b in work.values()) * B
+        ms_step = elapsed / K * 1e3
+        out = {
+            "metric": "training tiles/sec (fwd+bwd+update), default SRCNN 33x33, batch 4096/GPU",
+            "value": round(value, 1),
+            "unit": "tiles/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (smooth random 33x33 luma patches, seed 1234+rank; weights N(0,1e-3))",
+            "config": {"workload": "SRCNN default n1=64 n2=32 f1=9 f2=1 f3=5, fp32 training, "
+                                   "33x33 luma tiles, batch 4096 per GPU (BASELINE.json configs[1])",
+                       "global_batch": global_tiles, "tile": "33x33", "parallelism": "dp%d" % world,
+                       "kernel_path": args.path},
+            "roofline": roof,
+            "step_roofline": {"t_roof_ms": round(t_roof * 1e3, 4), "frac": round(t_roof * 1e3 / ms_step, 4)},
+            "kernels": kernels,
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(net_t, budget_s=args.cpu_budget)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,352 @@
+// abi.cpp -- extern "C" operator + network entry points of srcnn.h.
+//
+// Each operator validates its arguments the way the reference launcher does
+// (src/DataPipeline.cpp, src/LayerData.cpp:20-42), then dispatches: a gfx950
+// specialisation from ops_fast.hip when the shape matches and the path is
+// "auto", otherwise the shape-generic kernels of ops_generic.hip.  There is
+// no CPU fallback: every path launches HIP kernels.
+#include <algorithm>
+
+#include "common.hpp"
+#include "ops.hpp"
+
+using srcnn::as_stream;
+using srcnn::fail;
+
+namespace {
+
+bool fast_enabled() { return srcnn::g_path == 0; }
+
+int check_layer(const char* who, uint32_t n_prev, uint32_t n_cur, uint32_t f) {
+  SRCNN_REQUIRE(f > 0 && n_prev > 0 && n_cur > 0,
+                "%s: f(%u), n_prev_filter_cnt(%u) and current_filter_count(%u) must be > 0", who,
+                f, n_prev, n_cur);
+  return SRCNN_OK;
+}
+
+struct NetDims {
+  uint32_t w1, h1, w2, h2, w3, h3;
+  size_t s1, s2, s3;  // per-sample floats of A1, A2, A3
+};
+
+int net_dims(const srcnn_net* net, uint32_t w, uint32_t h, NetDims* d) {
+  SRCNN_REQUIRE(net, "null srcnn_net");
+  SRCNN_REQUIRE(net->n1 > 0 && net->n2 > 0, "n1(%u) and n2(%u) should be >0", net->n1, net->n2);
+  SRCNN_REQUIRE(net->f1 > 0 && net->f2 > 0 && net->f3 > 0 && (net->f1 & 1) && (net->f2 & 1) &&
+                    (net->f3 & 1),
+                "f1(%u), f2(%u), f3(%u) should be odd and >0 (Config.cpp:64-74)", net->f1,
+                net->f2, net->f3);
+  const uint32_t pad = net->f1 + net->f2 + net->f3 - 3;  // Config::total_padding
+  SRCNN_REQUIRE(w > pad && h > pad, "sample %ux%u is not larger than total padding %u", w, h, pad);
+  d->w1 = w - net->f1 + 1;
+  d->h1 = h - net->f1 + 1;
+  d->w2 = d->w1 - net->f2 + 1;
+  d->h2 = d->h1 - net->f2 + 1;
+  d->w3 = d->w2 - net->f3 + 1;
+  d->h3 = d->h2 - net->f3 + 1;
+  d->s1 = (size_t)d->w1 * d->h1 * net->n1;
+  d->s2 = (size_t)d->w2 * d->h2 * net->n2;
+  d->s3 = (size_t)d->w3 * d->h3;
+  return SRCNN_OK;
+}
+
+size_t align_up(size_t v) { return (v + 255) & ~size_t(255); }
+
+size_t grad_ws_bytes(uint32_t n_prev, uint32_t n_cur, uint32_t f, uint32_t ow, uint32_t oh,
+                     uint32_t batch) {
+  size_t b = 0;
+  if (fast_enabled()) b = srcnn::fast::grad_workspace_bytes(n_prev, n_cur, f, ow, oh, batch);
+  if (b == 0) b = srcnn::generic::grad_workspace_bytes(n_prev, n_cur, f, batch);
+  return b;
+}
+
+}  // namespace
+
+extern "C" {
+
+int srcnn_fill_f32(float* dst, float value, size_t count, srcnn_stream_t stream) {
+  if (count == 0) return SRCNN_OK;
+  SRCNN_REQUIRE(dst, "srcnn_fill_f32: null pointer");
+  return srcnn::fill(dst, value, count, as_stream(stream));
+}
+
+int srcnn_conv_fwd(const float* in, float* out, const float* W, const float* B, uint32_t in_w,
+                   uint32_t in_h, uint32_t n_prev, uint32_t n_cur, uint32_t f, int relu,
+                   uint32_t batch, srcnn_stream_t stream) {
+  if (int rc = check_layer("execute_layer", n_prev, n_cur, f)) return rc;
+  SRCNN_REQUIRE(in_w >= f && in_h >= f,
+                "execute_layer: input %ux%u smaller than filter f=%u", in_w, in_h, f);
+  if (batch == 0) return SRCNN_OK;
+  SRCNN_REQUIRE(in && out && W && B, "execute_layer: null buffer");
+  hipStream_t s = as_stream(stream);
+  if (fast_enabled()) {
+    int rc = srcnn::fast::try_conv_fwd(in, out, W, B, in_w, in_h, n_prev, n_cur, f, relu, batch, s);
+    if (rc != 0) return rc < 0 ? rc : SRCNN_OK;
+  }
+  return srcnn::generic::conv_fwd(in, out, W, B, in_w, in_h, n_prev, n_cur, f, relu, batch, s);
+}
+
+int srcnn_last_delta(const float* gt, const float* y, float* d, uint32_t gt_w, uint32_t gt_h,
+                     uint32_t out_w, uint32_t out_h, uint32_t batch, srcnn_stream_t stream) {
+  SRCNN_REQUIRE(out_w > 0 && out_h > 0 && gt_w >= out_w && gt_h >= out_h,
+                "last_layer_delta: ground truth %ux%u smaller than result %ux%u", gt_w, gt_h,
+                out_w, out_h);
+  if (batch == 0) return SRCNN_OK;
+  SRCNN_REQUIRE(gt && y && d, "last_layer_delta: null buffer");
+  return srcnn::generic::last_delta(gt, y, d, gt_w, gt_h, out_w, out_h, batch, as_stream(stream));
+}
+
+int srcnn_conv_delta(const float* d_next, const float* y_curr, float* d_curr,
+                     const float* W_next, uint32_t f_next, uint32_t n_curr, uint32_t n_next,
+                     uint32_t curr_w, uint32_t curr_h, uint32_t batch, srcnn_stream_t stream) {
+  if (int rc = check_layer("calculate_deltas", n_curr, n_next, f_next)) return rc;
+  SRCNN_REQUIRE(curr_w >= f_next && curr_h >= f_next,
+                "calculate_deltas: layer output %ux%u smaller than next filter f=%u", curr_w,
+                curr_h, f_next);
+  if (batch == 0) return SRCNN_OK;
+  SRCNN_REQUIRE(d_next && y_curr && d_curr && W_next, "calculate_deltas: null buffer");
+  hipStream_t s = as_stream(stream);
+  if (fast_enabled()) {
+    int rc = srcnn::fast::try_conv_delta(d_next, y_curr, d_curr, W_next, f_next, n_curr, n_next,
+                                         curr_w, curr_h, batch, s);
+    if (rc != 0) return rc < 0 ? rc : SRCNN_OK;
+  }
+  return srcnn::generic::conv_delta(d_next, y_curr, d_curr, W_next, f_next, n_curr, n_next,
+                                    curr_w, curr_h, batch, s);
+}
+
+size_t srcnn_conv_grad_workspace_bytes(uint32_t n_prev, uint32_t n_cur, uint32_t f,
+                                       uint32_t out_w, uint32_t out_h, uint32_t batch) {
+  if (!f || !n_prev || !n_cur || !batch) return 0;
+  return grad_ws_bytes(n_prev, n_cur, f, out_w, out_h, batch);
+}
+
+int srcnn_conv_grad_acc(const float* in, const float* delta, float* gW, float* gB,
+                        uint32_t n_prev, uint32_t n_cur, uint32_t f, uint32_t out_w,
+                        uint32_t out_h, uint32_t batch, void* ws, size_t ws_bytes,
+                        srcnn_stream_t stream) {
+  if (int rc = check_layer("backpropagate", n_prev, n_cur, f)) return rc;
+  SRCNN_REQUIRE(out_w > 0 && out_h > 0, "backpropagate: empty layer output %ux%u", out_w, out_h);
+  if (batch == 0) return SRCNN_OK;
+  SRCNN_REQUIRE(in && delta && gW && gB, "backpropagate: null buffer");
+  SRCNN_REQUIRE(ws, "backpropagate: null workspace (see srcnn_conv_grad_workspace_bytes)");
+  hipStream_t s = as_stream(stream);
+  if (fast_enabled()) {
+    int rc = srcnn::fast::try_conv_grad_acc(in, delta, gW, gB, n_prev, n_cur, f, out_w, out_h,
+                                            batch, ws, ws_bytes, s);
+    if (rc != 0) return rc < 0 ? rc : SRCNN_OK;
+  }
+  return srcnn::generic::conv_grad_acc(in, delta, gW, gB, n_prev, n_cur, f, out_w, out_h, batch,
+                                       ws, ws_bytes, s);
+}
+
+int srcnn_sgd_update(float* W, float* B, const float* gW, const float* gB, float* dW_prev,
+                     float* dB_prev, float momentum, float wd, float lr, uint32_t batch,
+                     uint32_t nW, uint32_t nB, srcnn_stream_t stream) {
+  SRCNN_REQUIRE(batch > 0, "update_parameters: batch size must be > 0");
+  SRCNN_REQUIRE(nB <= nW, "update_parameters: bias_size(%u) > weights_size(%u)", nB, nW);
+  if (nW == 0) return SRCNN_OK;
+  SRCNN_REQUIRE(W && gW && dW_prev && (nB == 0 || (B && gB && dB_prev)),
+                "update_parameters: null buffer");
+  return srcnn::sgd_update(W, B, gW, gB, dW_prev, dB_prev, momentum, wd, lr, batch, nW, nB,
+                           as_stream(stream));
+}
+
+size_t srcnn_reduce_workspace_bytes(size_t len) {
+  return (srcnn::reduce_blocks(len) + 1) * sizeof(float);
+}
+
+int srcnn_sq_err(const float* gt, const float* y, float* result, uint32_t gt_w, uint32_t gt_h,
+                 uint32_t out_w, uint32_t out_h, uint32_t batch, void* ws, size_t ws_bytes,
+                 srcnn_stream_t stream) {
+  SRCNN_REQUIRE(out_w > 0 && out_h > 0 && gt_w >= out_w && gt_h >= out_h,
+                "squared_error: ground truth %ux%u smaller than result %ux%u", gt_w, gt_h, out_w,
+                out_h);
+  SRCNN_REQUIRE(gt && y && result && ws, "squared_error: null buffer");
+  const size_t len = (size_t)batch * out_w * out_h;
+  if (len == 0) return srcnn::fill(result, 0.0f, 1, as_stream(stream));
+  return srcnn::reduce(2, y, gt, len, gt_w, gt_h, out_w, out_h, result, 0, ws, ws_bytes,
+                       as_stream(stream));
+}
+
+int srcnn_sum(const float* data, size_t len, int squared, float* result, void* ws,
+              size_t ws_bytes, srcnn_stream_t stream) {
+  SRCNN_REQUIRE(result && ws, "sum: null buffer");
+  if (len == 0) return srcnn::fill(result, 0.0f, 1, as_stream(stream));
+  SRCNN_REQUIRE(data, "sum: null data");
+  return srcnn::reduce(squared ? 1 : 0, data, nullptr, len, 0, 0, 0, 0, result, 0, ws, ws_bytes,
+                       as_stream(stream));
+}
+
+int srcnn_sub_scalar(float* data, float value, size_t len, srcnn_stream_t stream) {
+  if (len == 0) return SRCNN_OK;
+  SRCNN_REQUIRE(data, "subtract_from_all: null data");
+  return srcnn::sub_scalar(data, value, len, as_stream(stream));
+}
+
+int srcnn_sub_mean(float* data, size_t len, float* mean, void* ws, size_t ws_bytes,
+                   srcnn_stream_t stream) {
+  SRCNN_REQUIRE(len > 0 && data && ws, "subtract_mean: empty or null buffer");
+  return srcnn::sub_mean(data, len, mean, ws, ws_bytes, as_stream(stream));
+}
+
+int srcnn_extract_luma(const uint8_t* rgba, float* luma, uint32_t w, uint32_t h, int normalize,
+                       srcnn_stream_t stream) {
+  if ((size_t)w * h == 0) return SRCNN_OK;
+  SRCNN_REQUIRE(rgba && luma, "extract_luma: null buffer");
+  return srcnn::extract_luma(rgba, luma, w, h, normalize, as_stream(stream));
+}
+
+int srcnn_swap_luma(const uint8_t* rgba, const float* new_luma, uint8_t* rgb, uint32_t w,
+                    uint32_t h, uint32_t luma_w, uint32_t luma_h, srcnn_stream_t stream) {
+  SRCNN_REQUIRE(luma_w <= w && luma_h <= h, "swap_luma: luma %ux%u larger than image %ux%u",
+                luma_w, luma_h, w, h);
+  if ((size_t)w * h == 0) return SRCNN_OK;
+  SRCNN_REQUIRE(rgba && rgb && (new_luma || luma_w * luma_h == 0), "swap_luma: null buffer");
+  return srcnn::swap_luma(rgba, new_luma, rgb, w, h, luma_w, luma_h, as_stream(stream));
+}
+
+// ---------------------------------------------------------------------------
+// network level
+// ---------------------------------------------------------------------------
+int srcnn_net_offsets(const srcnn_net* net, size_t off[6]) {
+  SRCNN_REQUIRE(net && off, "srcnn_net_offsets: null argument");
+  off[0] = 0;
+  off[1] = off[0] + (size_t)net->f1 * net->f1 * net->n1;
+  off[2] = off[1] + net->n1;
+  off[3] = off[2] + (size_t)net->f2 * net->f2 * net->n1 * net->n2;
+  off[4] = off[3] + net->n2;
+  off[5] = off[4] + (size_t)net->f3 * net->f3 * net->n2;
+  return SRCNN_OK;
+}
+
+size_t srcnn_net_param_count(const srcnn_net* net) {
+  size_t off[6];
+  if (srcnn_net_offsets(net, off)) return 0;
+  return off[5] + 1;
+}
+
+size_t srcnn_train_workspace_bytes(const srcnn_net* net, uint32_t w, uint32_t h, uint32_t batch) {
+  NetDims d;
+  if (net_dims(net, w, h, &d) || batch == 0) return 0;
+  size_t b = 0;
+  b += 2 * align_up(d.s1 * batch * sizeof(float));  // A1, D1
+  b += 2 * align_up(d.s2 * batch * sizeof(float));  // A2, D2
+  b += 2 * align_up(d.s3 * batch * sizeof(float));  // A3, D3
+  size_t g = std::max({grad_ws_bytes(1, net->n1, net->f1, d.w1, d.h1, batch),
+                       grad_ws_bytes(net->n1, net->n2, net->f2, d.w2, d.h2, batch),
+                       grad_ws_bytes(net->n2, 1, net->f3, d.w3, d.h3, batch),
+                       srcnn_reduce_workspace_bytes(d.s3 * batch)});
+  return b + align_up(g);
+}
+
+int srcnn_train_fwd_bwd(const srcnn_net* net, const float* X, const float* T, uint32_t w,
+                        uint32_t h, uint32_t batch, const float* params, float* grads,
+                        float* sq_err, void* ws, size_t ws_bytes, srcnn_stream_t stream) {
+  NetDims d;
+  if (int rc = net_dims(net, w, h, &d)) return rc;
+  if (batch == 0) return SRCNN_OK;
+  SRCNN_REQUIRE(X && T && params && grads && ws, "train_fwd_bwd: null buffer");
+  const size_t need = srcnn_train_workspace_bytes(net, w, h, batch);
+  if (ws_bytes < need)
+    return fail(SRCNN_ERR_WORKSPACE, "train_fwd_bwd: workspace %zu B < %zu B", ws_bytes, need);
+  size_t off[6];
+  srcnn_net_offsets(net, off);
+  char* p = static_cast<char*>(ws);
+  float* A1 = reinterpret_cast<float*>(p);
+  p += align_up(d.s1 * batch * sizeof(float));
+  float* D1 = reinterpret_cast<float*>(p);
+  p += align_up(d.s1 * batch * sizeof(float));
+  float* A2 = reinterpret_cast<float*>(p);
+  p += align_up(d.s2 * batch * sizeof(float));
+  float* D2 = reinterpret_cast<float*>(p);
+  p += align_up(d.s2 * batch * sizeof(float));
+  float* A3 = reinterpret_cast<float*>(p);
+  p += align_up(d.s3 * batch * sizeof(float));
+  float* D3 = reinterpret_cast<float*>(p);
+  p += align_up(d.s3 * batch * sizeof(float));
+  void* gws = p;
+  const size_t gws_bytes = ws_bytes - (size_t)(p - static_cast<char*>(ws));
+  const float *W1 = params + off[0], *B1 = params + off[1], *W2 = params + off[2],
+              *B2 = params + off[3], *W3 = params + off[4], *B3 = params + off[5];
+  float *gW1 = grads + off[0], *gB1 = grads + off[1], *gW2 = grads + off[2],
+        *gB2 = grads + off[3], *gW3 = grads + off[4], *gB3 = grads + off[5];
+  int rc;
+  // forward: ConfigBasedDataPipeline.cpp:375-397
+  if ((rc = srcnn_conv_fwd(X, A1, W1, B1, w, h, 1, net->n1, net->f1, 1, batch, stream))) return rc;
+  if ((rc = srcnn_conv_fwd(A1, A2, W2, B2, d.w1, d.h1, net->n1, net->n2, net->f2, 1, batch, stream)))
+    return rc;
+  if ((rc = srcnn_conv_fwd(A2, A3, W3, B3, d.w2, d.h2, net->n2, 1, net->f3, 0, batch, stream)))
+    return rc;
+  if (sq_err &&
+      (rc = srcnn::reduce(2, A3, T, d.s3 * batch, w, h, d.w3, d.h3, sq_err, 1, gws, gws_bytes,
+                          srcnn::as_stream(stream))))
+    return rc;
+  // backward: ConfigBasedDataPipeline.cpp:420-479
+  if ((rc = srcnn_last_delta(T, A3, D3, w, h, d.w3, d.h3, batch, stream))) return rc;
+  if ((rc = srcnn_conv_delta(D3, A2, D2, W3, net->f3, net->n2, 1, d.w2, d.h2, batch, stream)))
+    return rc;
+  if ((rc = srcnn_conv_delta(D2, A1, D1, W2, net->f2, net->n1, net->n2, d.w1, d.h1, batch, stream)))
+    return rc;
+  if ((rc = srcnn_conv_grad_acc(A2, D3, gW3, gB3, net->n2, 1, net->f3, d.w3, d.h3, batch, gws,
+                                gws_bytes, stream)))
+    return rc;
+  if ((rc = srcnn_conv_grad_acc(A1, D2, gW2, gB2, net->n1, net->n2, net->f2, d.w2, d.h2, batch,
+                                gws, gws_bytes, stream)))
+    return rc;
+  return srcnn_conv_grad_acc(X, D1, gW1, gB1, 1, net->n1, net->f1, d.w1, d.h1, batch, gws,
+                             gws_bytes, stream);
+}
+
+int srcnn_update_all(const srcnn_net* net, float* params, float* grads, float* momentum_bufs,
+                     float momentum, float wd, const float* lr, uint32_t batch,
+                     srcnn_stream_t stream) {
+  SRCNN_REQUIRE(net && params && grads && momentum_bufs && lr, "update_all: null argument");
+  size_t off[6];
+  srcnn_net_offsets(net, off);
+  const size_t total = off[5] + 1;
+  // layer 3, 2, 1: ConfigBasedDataPipeline.cpp:491-508
+  for (int l = 2; l >= 0; l--) {
+    const size_t wo = off[2 * l], bo = off[2 * l + 1];
+    const size_t end = l == 2 ? total : off[2 * l + 2];
+    int rc = srcnn_sgd_update(params + wo, params + bo, grads + wo, grads + bo,
+                              momentum_bufs + wo, momentum_bufs + bo, momentum, wd, lr[l], batch,
+                              (uint32_t)(bo - wo), (uint32_t)(end - bo), stream);
+    if (rc) return rc;
+  }
+  return srcnn::fill(grads, 0.0f, total, srcnn::as_stream(stream));  // :511-517
+}
+
+size_t srcnn_forward_workspace_bytes(const srcnn_net* net, uint32_t w, uint32_t h,
+                                     uint32_t batch) {
+  NetDims d;
+  if (net_dims(net, w, h, &d) || batch == 0) return 0;
+  return align_up(d.s1 * batch * sizeof(float)) + align_up(d.s2 * batch * sizeof(float));
+}
+
+int srcnn_forward(const srcnn_net* net, const float* X, uint32_t w, uint32_t h, uint32_t batch,
+                  const float* params, float* out, void* ws, size_t ws_bytes,
+                  srcnn_stream_t stream) {
+  NetDims d;
+  if (int rc = net_dims(net, w, h, &d)) return rc;
+  if (batch == 0) return SRCNN_OK;
+  SRCNN_REQUIRE(X && params && out && ws, "forward: null buffer");
+  const size_t need = srcnn_forward_workspace_bytes(net, w, h, batch);
+  if (ws_bytes < need)
+    return fail(SRCNN_ERR_WORKSPACE, "forward: workspace %zu B < %zu B", ws_bytes, need);
+  size_t off[6];
+  srcnn_net_offsets(net, off);
+  float* A1 = static_cast<float*>(ws);
+  float* A2 = reinterpret_cast<float*>(static_cast<char*>(ws) + align_up(d.s1 * batch * sizeof(float)));
+  int rc;
+  if ((rc = srcnn_conv_fwd(X, A1, params + off[0], params + off[1], w, h, 1, net->n1, net->f1, 1,
+                           batch, stream)))
+    return rc;
+  if ((rc = srcnn_conv_fwd(A1, A2, params + off[2], params + off[3], d.w1, d.h1, net->n1, net->n2,
+                           net->f2, 1, batch, stream)))
+    return rc;
+  return srcnn_conv_fwd(A2, out, params + off[4], params + off[5], d.w2, d.h2, net->n2, 1,
+                        net->f3, 0, batch, stream);
+}
+
+}  // extern "C"

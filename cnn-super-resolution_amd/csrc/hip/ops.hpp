@@ -1,0 +1,57 @@
+// ops.hpp -- internal launchers behind srcnn.h (no validation here; abi.cpp
+// validates shapes exactly once, then dispatches generic vs gfx950 paths).
+#pragma once
+
+#include "common.hpp"
+
+namespace srcnn {
+
+namespace generic {
+int conv_fwd(const float* in, float* out, const float* W, const float* B, uint32_t in_w,
+             uint32_t in_h, uint32_t n_prev, uint32_t n_cur, uint32_t f, int relu,
+             uint32_t batch, hipStream_t s);
+int last_delta(const float* gt, const float* y, float* d, uint32_t gt_w, uint32_t gt_h,
+               uint32_t out_w, uint32_t out_h, uint32_t batch, hipStream_t s);
+int conv_delta(const float* d_next, const float* y_curr, float* d_curr, const float* W_next,
+               uint32_t f_next, uint32_t n_curr, uint32_t n_next, uint32_t curr_w,
+               uint32_t curr_h, uint32_t batch, hipStream_t s);
+size_t grad_workspace_bytes(uint32_t n_prev, uint32_t n_cur, uint32_t f, uint32_t batch);
+int conv_grad_acc(const float* in, const float* d, float* gW, float* gB, uint32_t n_prev,
+                  uint32_t n_cur, uint32_t f, uint32_t out_w, uint32_t out_h, uint32_t batch,
+                  void* ws, size_t ws_bytes, hipStream_t s);
+}  // namespace generic
+
+// gfx950 specialisations (ops_fast.hip).  Each `try_*` returns 1 when it
+// handled the call, 0 when the shape is not specialised, <0 on error.
+namespace fast {
+int try_conv_fwd(const float* in, float* out, const float* W, const float* B, uint32_t in_w,
+                 uint32_t in_h, uint32_t n_prev, uint32_t n_cur, uint32_t f, int relu,
+                 uint32_t batch, hipStream_t s);
+int try_conv_delta(const float* d_next, const float* y_curr, float* d_curr, const float* W_next,
+                   uint32_t f_next, uint32_t n_curr, uint32_t n_next, uint32_t curr_w,
+                   uint32_t curr_h, uint32_t batch, hipStream_t s);
+// workspace the fast gradient path needs for this shape (0 = not specialised)
+size_t grad_workspace_bytes(uint32_t n_prev, uint32_t n_cur, uint32_t f, uint32_t out_w,
+                            uint32_t out_h, uint32_t batch);
+int try_conv_grad_acc(const float* in, const float* d, float* gW, float* gB, uint32_t n_prev,
+                      uint32_t n_cur, uint32_t f, uint32_t out_w, uint32_t out_h,
+                      uint32_t batch, void* ws, size_t ws_bytes, hipStream_t s);
+}  // namespace fast
+
+int sgd_update(float* W, float* B, const float* gW, const float* gB, float* dW, float* dB,
+               float mu, float wd, float lr, uint32_t batch, uint32_t nW, uint32_t nB,
+               hipStream_t s);
+uint32_t reduce_blocks(size_t len);
+// mode 0 sum, 1 sum of squares, 2 squared error (gt/out dims used only by mode 2)
+int reduce(int mode, const float* a, const float* gt, size_t len, uint32_t gt_w, uint32_t gt_h,
+           uint32_t out_w, uint32_t out_h, float* result, int accumulate, void* ws,
+           size_t ws_bytes, hipStream_t s);
+int sub_scalar(float* d, float v, size_t len, hipStream_t s);
+int sub_mean(float* d, size_t len, float* mean_out, void* ws, size_t ws_bytes, hipStream_t s);
+int fill(float* d, float v, size_t n, hipStream_t s);
+int extract_luma(const uint8_t* rgba, float* luma, uint32_t w, uint32_t h, int normalize,
+                 hipStream_t s);
+int swap_luma(const uint8_t* rgba, const float* nl, uint8_t* rgb, uint32_t w, uint32_t h,
+              uint32_t lw, uint32_t lh, hipStream_t s);
+
+}  // namespace srcnn

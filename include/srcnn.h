@@ -1,0 +1,225 @@
+/*
+ * srcnn.h -- C ABI of libsrcnn_hip.so, the MI355X (gfx950) SRCNN hot path.
+ *
+ * This is the drop-in boundary that replaces the reference's host/device
+ * boundary (clEnqueue* inside src/opencl/Context.cpp and src/opencl/Kernel.cpp
+ * of Scthe/cnn-Super-Resolution).  Plain pointers and sizes only; every
+ * device pointer is HBM memory of the current device; every call is
+ * stream-ordered on `stream` (a hipStream_t, NULL = the default stream).
+ *
+ * Numerics: fp32 throughout, same layouts as the reference:
+ *   activations per-sample HWC  idx = s*C*W*H + (y*W + x)*C + c
+ *               (src/kernel/layer_uber_kernel.cl:51-56)
+ *   weights     W[dy][dx][c_in][c_out], c_out innermost
+ *               (src/kernel/layer_uber_kernel.cl:3-13)
+ *   flat net    [W1|B1|W2|B2|W3|B3] (one buffer, so one all-reduce covers
+ *               every gradient; the per-layer LayerAllocationPool handles of
+ *               src/DataPipeline.hpp:11-29 are views into it)
+ *
+ * Errors: every int-returning function returns SRCNN_OK (0) or a negative
+ * SRCNN_ERR_*; srcnn_last_error() then holds a thread-local message.  Shape
+ * validation mirrors the reference's runtime_error checks
+ * (src/LayerData.cpp:20-42, src/DataPipeline.cpp:339-356, :62-86).
+ *
+ * Gradients are reduced deterministically (no float atomics): the racy
+ * `target_grad_w[id] += grad_w` of src/kernel/backpropagate.cl:110 is
+ * replaced by per-sample partial sums added in sample order.
+ */
+#ifndef SRCNN_H
+#define SRCNN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SRCNN_API __attribute__((visibility("default")))
+#define SRCNN_ABI_VERSION 1
+
+enum {
+  SRCNN_OK = 0,
+  SRCNN_ERR_INVALID = -1,   /* bad shape / argument (reference: std::runtime_error) */
+  SRCNN_ERR_HIP = -2,       /* HIP runtime failure (reference: check_error, Context.cpp:111-119) */
+  SRCNN_ERR_WORKSPACE = -3, /* workspace smaller than the matching *_workspace_bytes() */
+  SRCNN_ERR_ALLOC = -4      /* device allocation failed */
+};
+
+typedef void* srcnn_stream_t; /* hipStream_t */
+typedef void* srcnn_event_t;  /* hipEvent_t  */
+
+SRCNN_API int srcnn_abi_version(void);
+SRCNN_API const char* srcnn_last_error(void);
+
+/* ---- runtime: replaces opencl::Context (src/opencl/Context.hpp:72-299) ---- */
+SRCNN_API int srcnn_device_count(int* count);
+SRCNN_API int srcnn_set_device(int device);                 /* Context::init, Context.cpp:45-79 */
+SRCNN_API int srcnn_device_name(char* buf, size_t len);
+SRCNN_API int srcnn_malloc(void** ptr, size_t bytes);       /* Context::allocate, Context.cpp:164-176 */
+SRCNN_API int srcnn_free(void* ptr);                        /* RawMemoryHandle::release, Context.cpp:26-33 */
+/* blocking H2D / D2H (write_buffer / read_buffer with block=true, Context.cpp:235-290) */
+SRCNN_API int srcnn_memcpy_h2d(void* dst, const void* src, size_t bytes, srcnn_stream_t stream);
+SRCNN_API int srcnn_memcpy_d2h(void* dst, const void* src, size_t bytes, srcnn_stream_t stream);
+/* async D2D (copy_buffer, Context.cpp:312-341) */
+SRCNN_API int srcnn_memcpy_d2d(void* dst, const void* src, size_t bytes, srcnn_stream_t stream);
+/* async fill (zeros_float / fill_float, Context.cpp:292-310; no host vector) */
+SRCNN_API int srcnn_fill_f32(float* dst, float value, size_t count, srcnn_stream_t stream);
+SRCNN_API int srcnn_stream_create(srcnn_stream_t* stream);
+SRCNN_API int srcnn_stream_destroy(srcnn_stream_t stream);
+SRCNN_API int srcnn_stream_sync(srcnn_stream_t stream);     /* Context::block, Context.cpp:153-162 */
+SRCNN_API int srcnn_device_sync(void);
+SRCNN_API int srcnn_event_create(srcnn_event_t* ev);
+SRCNN_API int srcnn_event_destroy(srcnn_event_t ev);
+SRCNN_API int srcnn_event_record(srcnn_event_t ev, srcnn_stream_t stream);
+SRCNN_API int srcnn_event_sync(srcnn_event_t ev);
+SRCNN_API int srcnn_event_elapsed_ms(srcnn_event_t start, srcnn_event_t stop, float* ms);
+
+/* ---- operators: one per reference L3 launcher (src/DataPipeline.hpp:62-175) ---- */
+
+/* DataPipeline::execute_layer (src/DataPipeline.cpp:358-410) running kernel
+ * `forward` (src/kernel/layer_uber_kernel.cl:36-96): valid correlation
+ * f x f x n_prev -> n_cur, + bias, ReLU unless relu == 0 (SKIP_RELU).
+ * in: [batch][in_h][in_w][n_prev]  out: [batch][in_h-f+1][in_w-f+1][n_cur] */
+SRCNN_API int srcnn_conv_fwd(const float* in, float* out, const float* W,
+                             const float* B, uint32_t in_w, uint32_t in_h,
+                             uint32_t n_prev, uint32_t n_cur, uint32_t f,
+                             int relu, uint32_t batch, srcnn_stream_t stream);
+
+/* DataPipeline::last_layer_delta (src/DataPipeline.cpp:474-520), kernel
+ * src/kernel/last_layer_delta.cl:14-50: d = (y - gt_centre) * [y > 0]. */
+SRCNN_API int srcnn_last_delta(const float* gt, const float* y, float* d,
+                               uint32_t gt_w, uint32_t gt_h, uint32_t out_w,
+                               uint32_t out_h, uint32_t batch,
+                               srcnn_stream_t stream);
+
+/* DataPipeline::calculate_deltas (src/DataPipeline.cpp:522-594), kernel
+ * src/kernel/layer_deltas.cl:42-127:
+ *   d_curr[y,x,n] = [y_curr>0] * sum_{dy,dx,k} d_next[y-dy,x-dx,k] * W_next[dy,dx,n,k]
+ * y_curr, d_curr: [batch][curr_h][curr_w][n_curr]
+ * d_next:         [batch][curr_h-f_next+1][curr_w-f_next+1][n_next] */
+SRCNN_API int srcnn_conv_delta(const float* d_next, const float* y_curr,
+                               float* d_curr, const float* W_next,
+                               uint32_t f_next, uint32_t n_curr,
+                               uint32_t n_next, uint32_t curr_w,
+                               uint32_t curr_h, uint32_t batch,
+                               srcnn_stream_t stream);
+
+/* DataPipeline::backpropagate (src/DataPipeline.cpp:596-663), kernel
+ * src/kernel/backpropagate.cl:56-114: ACCUMULATES (+=) into gW / gB
+ *   gW[dy,dx,k,n] += sum_s sum_{y,x} in_s[y+dy,x+dx,k] * d_s[y,x,n]
+ *   gB[n]         += sum_s sum_{y,x} d_s[y,x,n]
+ * in: [batch][out_h+f-1][out_w+f-1][n_prev]   d: [batch][out_h][out_w][n_cur] */
+SRCNN_API size_t srcnn_conv_grad_workspace_bytes(uint32_t n_prev, uint32_t n_cur,
+                                                 uint32_t f, uint32_t out_w,
+                                                 uint32_t out_h, uint32_t batch);
+SRCNN_API int srcnn_conv_grad_acc(const float* in, const float* delta,
+                                  float* gW, float* gB, uint32_t n_prev,
+                                  uint32_t n_cur, uint32_t f, uint32_t out_w,
+                                  uint32_t out_h, uint32_t batch, void* ws,
+                                  size_t ws_bytes, srcnn_stream_t stream);
+
+/* DataPipeline::update_parameters (src/DataPipeline.cpp:665-729), kernel
+ * src/kernel/update_parameters.cl:1-33:
+ *   dW = mu*dW_prev + lr*gW + wd*W;  W -= dW / batch;  dW_prev = dW
+ *   dB = mu*dB_prev + lr*gB;         B -= dB / batch;  dB_prev = dB */
+SRCNN_API int srcnn_sgd_update(float* W, float* B, const float* gW,
+                               const float* gB, float* dW_prev,
+                               float* dB_prev, float momentum, float wd,
+                               float lr, uint32_t batch, uint32_t nW,
+                               uint32_t nB, srcnn_stream_t stream);
+
+/* Deterministic reductions: DataPipeline::squared_error (src/DataPipeline.cpp:416-472,
+ * kernel squared_error.cl:36-92) and DataPipeline::sum (:282-313, sum.cl:35-68).
+ * The scalar result is written to device memory `result`. */
+SRCNN_API size_t srcnn_reduce_workspace_bytes(size_t len);
+SRCNN_API int srcnn_sq_err(const float* gt, const float* y, float* result,
+                           uint32_t gt_w, uint32_t gt_h, uint32_t out_w,
+                           uint32_t out_h, uint32_t batch, void* ws,
+                           size_t ws_bytes, srcnn_stream_t stream);
+SRCNN_API int srcnn_sum(const float* data, size_t len, int squared,
+                        float* result, void* ws, size_t ws_bytes,
+                        srcnn_stream_t stream);
+/* DataPipeline::subtract_from_all (src/DataPipeline.cpp:315-333) */
+SRCNN_API int srcnn_sub_scalar(float* data, float value, size_t len,
+                               srcnn_stream_t stream);
+/* DataPipeline::subtract_mean (src/DataPipeline.cpp:268-280) without the
+ * host round trip: mean = sum/len computed and subtracted on the device,
+ * also stored to `mean` (device, may be NULL). */
+SRCNN_API int srcnn_sub_mean(float* data, size_t len, float* mean, void* ws,
+                             size_t ws_bytes, srcnn_stream_t stream);
+/* DataPipeline::extract_luma (src/DataPipeline.cpp:186-220, extract_luma.cl:7-23):
+ * rgba [h][w][4] u8 -> luma [h][w] f32 (/255 if normalize). */
+SRCNN_API int srcnn_extract_luma(const uint8_t* rgba, float* luma, uint32_t w,
+                                 uint32_t h, int normalize,
+                                 srcnn_stream_t stream);
+/* DataPipeline::swap_luma (src/DataPipeline.cpp:222-266, swap_luma.cl:18-69):
+ * new luma (centre luma_w x luma_h) + original CbCr -> rgb [h][w][3] u8. */
+SRCNN_API int srcnn_swap_luma(const uint8_t* rgba, const float* new_luma,
+                              uint8_t* rgb, uint32_t w, uint32_t h,
+                              uint32_t luma_w, uint32_t luma_h,
+                              srcnn_stream_t stream);
+
+/* ---- network level: ConfigBasedDataPipeline (src/ConfigBasedDataPipeline.cpp) ---- */
+typedef struct srcnn_net {
+  uint32_t n1, n2, f1, f2, f3; /* Config n1,n2,f1,f2,f3 (src/Config.hpp:402-403) */
+} srcnn_net;
+
+/* offsets (in floats) of W1,B1,W2,B2,W3,B3 inside the flat parameter buffer */
+SRCNN_API int srcnn_net_offsets(const srcnn_net* net, size_t offsets[6]);
+SRCNN_API size_t srcnn_net_param_count(const srcnn_net* net);
+
+/* One chunk of ConfigBasedDataPipeline::execute_batch(backpropagate=true)
+ * (src/ConfigBasedDataPipeline.cpp:287-355): forward L1..L3 (:359-400),
+ * last-layer delta, deltas and gradients (:402-482).  Gradients are
+ * ACCUMULATED into `grads` (flat layout).  X = mean-subtracted input luma,
+ * T = ground-truth luma, both [batch][h][w].  If sq_err != NULL the chunk's
+ * squared error (validation metric) is ADDED to *sq_err (device). */
+SRCNN_API size_t srcnn_train_workspace_bytes(const srcnn_net* net, uint32_t w,
+                                             uint32_t h, uint32_t batch);
+SRCNN_API int srcnn_train_fwd_bwd(const srcnn_net* net, const float* X,
+                                  const float* T, uint32_t w, uint32_t h,
+                                  uint32_t batch, const float* params,
+                                  float* grads, float* sq_err, void* ws,
+                                  size_t ws_bytes, srcnn_stream_t stream);
+
+/* ConfigBasedDataPipeline::update_parameters (src/ConfigBasedDataPipeline.cpp:484-520):
+ * update all layers with per-layer lr[3], shared momentum / wd, then zero
+ * the gradient accumulators (:511-517). */
+SRCNN_API int srcnn_update_all(const srcnn_net* net, float* params,
+                               float* grads, float* momentum_bufs,
+                               float momentum, float wd, const float* lr,
+                               uint32_t batch, srcnn_stream_t stream);
+
+/* Forward / inference (src/ConfigBasedDataPipeline.cpp:273-285, :359-400):
+ * out = A3 [batch][h-pad][w-pad], pad = f1+f2+f3-3. */
+SRCNN_API size_t srcnn_forward_workspace_bytes(const srcnn_net* net,
+                                               uint32_t w, uint32_t h,
+                                               uint32_t batch);
+SRCNN_API int srcnn_forward(const srcnn_net* net, const float* X, uint32_t w,
+                            uint32_t h, uint32_t batch, const float* params,
+                            float* out, void* ws, size_t ws_bytes,
+                            srcnn_stream_t stream);
+
+/* ---- profiling: the reference's `profile` mode (src/opencl/Kernel.cpp:108-116,
+ * src/opencl/Context.cpp:88-96) without blocking per launch: when enabled,
+ * every kernel launch is bracketed by a pair of hipEvents on its stream;
+ * srcnn_profile_count() waits for the recorded events and folds them into
+ * per-kernel totals. ---- */
+SRCNN_API int srcnn_profile_enable(int on);
+SRCNN_API int srcnn_profile_reset(void);
+SRCNN_API int srcnn_profile_count(int* n_kernels);
+SRCNN_API int srcnn_profile_get(int index, char* name, size_t name_len,
+                                uint64_t* launches, double* total_ms);
+/* prints "Kernel '<name>' total execution time: <ns>ns = <s>s" per kernel */
+SRCNN_API int srcnn_profile_print(void);
+
+/* Kernel-path selection (for A/B measurement and parity tests):
+ * 0 = auto (fast specialisations where the shape matches), 1 = generic only. */
+SRCNN_API int srcnn_set_path(int path);
+SRCNN_API int srcnn_get_path(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SRCNN_H */

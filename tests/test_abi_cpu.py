@@ -1,0 +1,101 @@
+"""CPU-side checks of the C-ABI library (no GPU compute): it loads, exports
+every symbol include/srcnn.h declares, and its host-only entry points
+(shape validation, sizes, offsets) behave like the reference's launchers."""
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "srcnn.h")
+LIB = os.path.join(ROOT, "cnn-super-resolution_amd", "lib", "libsrcnn_hip.so")
+
+
+def declared_symbols():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"SRCNN_API\s+[\w\s\*]+?\b(srcnn_\w+)\s*\(", src)))
+
+
+@pytest.fixture(scope="module")
+def S():
+    import srcnn_amd
+    return srcnn_amd
+
+
+def test_header_declares_api():
+    syms = declared_symbols()
+    assert len(syms) >= 40
+    for must in ("srcnn_conv_fwd", "srcnn_conv_delta", "srcnn_conv_grad_acc", "srcnn_sgd_update",
+                 "srcnn_last_delta", "srcnn_train_fwd_bwd", "srcnn_update_all", "srcnn_forward"):
+        assert must in syms
+
+
+def test_library_exports_every_declared_symbol(S):
+    out = subprocess.check_output(["nm", "-D", "--defined-only", LIB]).decode()
+    exported = set(re.findall(r"\bT\s+(srcnn_\w+)", out))
+    missing = [s for s in declared_symbols() if s not in exported]
+    assert not missing, missing
+    # no stray exports beyond the header (visibility=hidden elsewhere)
+    assert exported == set(declared_symbols())
+
+
+def test_binding_covers_header(S):
+    assert set(S.exported_symbols()) == set(declared_symbols())
+
+
+def test_abi_version(S):
+    assert S.abi_version() == 1
+
+
+def test_net_layout(S):
+    net = S.Net(64, 32, 9, 1, 5)
+    assert S.net_offsets(net) == [0, 5184, 5248, 7296, 7328, 8128]
+    assert S.net_param_count(net) == 8129            # 8,129 floats
+    wide = S.Net(128, 64, 9, 5, 5)
+    assert S.net_param_count(wide) == 216961         # 216,961 floats
+
+
+def test_workspace_queries(S):
+    net = S.Net(64, 32, 9, 1, 5)
+    b = S.train_workspace_bytes(net, 33, 33, 4096)
+    # at least A1,D1 (40000 f32) + A2,D2 (20000) + A3,D3 (441) per tile
+    assert b >= 4096 * 4 * (2 * 40000 + 2 * 20000 + 2 * 441)
+    assert S.forward_workspace_bytes(net, 256, 256, 1) >= 4 * (248 * 248 * 64 + 248 * 248 * 32)
+    assert S.conv_grad_workspace_bytes(1, 64, 9, 25, 25, 16) > 0
+    assert S.reduce_workspace_bytes(10 ** 6) >= 8
+    assert S.train_workspace_bytes(S.Net(64, 32, 9, 2, 5), 33, 33, 1) == 0  # invalid net
+
+
+@pytest.mark.parametrize("call", [
+    lambda S: S.conv_fwd(0, 0, 0, 0, 5, 5, 1, 3, 0, 1, 1),        # f = 0
+    lambda S: S.conv_fwd(0, 0, 0, 0, 3, 3, 1, 3, 5, 1, 1),        # input smaller than f
+    lambda S: S.conv_fwd(0, 0, 0, 0, 9, 9, 1, 3, 3, 1, 1),        # null buffers
+    lambda S: S.conv_delta(0, 0, 0, 0, 3, 0, 3, 5, 5, 1),         # n_curr = 0
+    lambda S: S.conv_grad_acc(0, 0, 0, 0, 0, 3, 3, 3, 3, 1, 0, 0),
+    lambda S: S.last_delta(0, 0, 0, 4, 4, 6, 6, 1),               # gt smaller than result
+    lambda S: S.sgd_update(0, 0, 0, 0, 0, 0, .9, 0., 1e-3, 0, 10, 1),  # batch 0
+    lambda S: S.sgd_update(0, 0, 0, 0, 0, 0, .9, 0., 1e-3, 1, 1, 10),  # bias > weights
+    lambda S: S.swap_luma(0, 0, 0, 4, 4, 8, 8),
+], ids=["f0", "small_input", "null", "n0", "grad_n0", "gt_small", "batch0", "bias_gt_w", "luma_big"])
+def test_validation_errors_without_gpu(S, call):
+    """Shape checks run on the host before any launch (DataPipeline.cpp:339-356, LayerData.cpp:20-42)."""
+    with pytest.raises(S.SrcnnError) as e:
+        call(S)
+    assert e.value.code == S.ERR_INVALID
+    assert S.last_error()
+
+
+def test_empty_batches_are_noops(S):
+    S.conv_fwd(0, 0, 0, 0, 9, 9, 1, 3, 3, 1, 0)
+    S.conv_delta(0, 0, 0, 0, 3, 2, 3, 5, 5, 0)
+    S.last_delta(0, 0, 0, 8, 8, 6, 6, 0)
+
+
+def test_path_switch(S):
+    S.set_path(1)
+    assert S.get_path() == 1
+    S.set_path(0)
+    with pytest.raises(S.SrcnnError):
+        S.set_path(7)

@@ -1,0 +1,409 @@
+"""GPU parity: the HIP path (called through the C ABI) against the CPU oracle
+and the reference's golden vectors.
+
+Tolerance: fp32, normwise 1e-4 (hip_util.RTOL) unless a fixture's own
+printed precision is coarser (then that precision, as in
+test_oracle_golden.py).  Integer / byte outputs (swap_luma) are exact.
+Every parametrised case runs on both kernel paths: "auto" (gfx950
+specialisations where the shape matches) and "generic".
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import srcnn_oracle as orc
+from conftest import GOLDEN
+from hip_util import RTOL, assert_close, make_batch, make_params
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def S():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import srcnn_amd
+    return srcnn_amd
+
+
+@pytest.fixture(params=[0, 1], ids=["auto", "generic"])
+def path(request, S):
+    S.set_path(request.param)
+    yield request.param
+    S.set_path(0)
+
+
+def load(name):
+    with open(os.path.join(GOLDEN, name)) as fh:
+        return json.load(fh)
+
+
+def D(a, dtype=np.float32):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=dtype)).cuda()
+
+
+def H(t):
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+def zeros(n, dtype=torch.float32):
+    return torch.zeros(int(n), dtype=dtype, device="cuda")
+
+
+# ----------------------------------------------------------------------------
+# the reference's own specs, through the HIP path
+# ----------------------------------------------------------------------------
+@pytest.mark.parametrize("case", sorted(load("layer_test_cases.json").keys()))
+def test_layer_spec(S, path, case):
+    d = load("layer_test_cases.json")[case]
+    f, k, n = d["f_spatial_size"], d["n_prev_filter_cnt"], d["current_filter_count"]
+    ow, oh = d["input_w"] - f + 1, d["input_h"] - f + 1
+    out = zeros(ow * oh * n)
+    S.conv_fwd(D(d["input"]), out, D(d["weights"]), D(d["bias"]), d["input_w"], d["input_h"], k, n,
+               f, 1, 1)
+    np.testing.assert_allclose(H(out), d["output"], rtol=0, atol=5e-4)
+
+
+def test_layer_deltas_spec(S, path):
+    d = load("layer_deltas.json")
+    y = np.maximum(np.array(d["input_x"], np.float32), 0)
+    out = zeros(50)
+    S.conv_delta(D(d["deltas"]), D(y), out, D(d["weights"]), d["f_next"], d["n_prev_layer"],
+                 d["n_next"], d["curr_w"], d["curr_h"], 1)
+    np.testing.assert_allclose(H(out), d["expected"], rtol=0, atol=2e-6)
+
+
+def test_backpropagation_spec(S, path):
+    d = load("backprop.json")
+    gW = D(np.full(54, d["grad_w_init"], np.float32))
+    gB = zeros(3)
+    ow = d["in_w"] - d["f"] + 1
+    nbytes = S.conv_grad_workspace_bytes(2, 3, 3, ow, ow, 1)
+    ws = zeros(nbytes // 4 + 1)
+    S.conv_grad_acc(D(d["input"]), D(d["deltas"]), gW, gB, 2, 3, 3, ow, ow, 1, ws, nbytes)
+    np.testing.assert_allclose(H(gW), d["expected_grad_w"], rtol=0, atol=6e-5)
+    np.testing.assert_allclose(H(gB), d["expected_grad_b"], rtol=0, atol=6e-4)
+
+
+def test_backpropagation_big_data(S, path):
+    """BackpropagationTest.cpp:534-546 (1024x1024, 32->16, f=3): crash-only in
+    the reference; here checked against the oracle on random data."""
+    rng = np.random.default_rng(11)
+    n_prev, n_cur, f, iw = 32, 16, 3, 1024
+    ow = iw - f + 1
+    inp = rng.standard_normal(iw * iw * n_prev).astype(np.float32)
+    dl = rng.standard_normal(ow * ow * n_cur).astype(np.float32)
+    nbytes = S.conv_grad_workspace_bytes(n_prev, n_cur, f, ow, ow, 1)
+    ws = zeros(nbytes // 4 + 1)
+    gW, gB = zeros(f * f * n_prev * n_cur), zeros(n_cur)
+    S.conv_grad_acc(D(inp), D(dl), gW, gB, n_prev, n_cur, f, ow, ow, 1, ws, nbytes)
+    rW, rB = orc.conv_grad_acc(inp, dl, np.zeros(f * f * n_prev * n_cur), np.zeros(n_cur), n_prev,
+                               n_cur, f, ow, ow, 1)
+    assert_close(H(gW), rW, 2e-4, "gW big data")   # 1M-term fp32 sums
+    assert_close(H(gB), rB, 2e-4, "gB big data")
+
+
+def test_update_parameters_spec(S):
+    rng = np.random.default_rng(1234)
+    nW, nB, batch = 5 * 5 * 2 * 400, 400, 2
+    vals = {}
+    for key, size in (("w", nW), ("b", nB)):
+        cur = (rng.integers(0, 2560, size) / 10.0).astype(np.float32)
+        grad = (rng.integers(0, 2560, size) / 100.0).astype(np.float32)
+        prev = (rng.integers(0, 2560, size) / 10.0).astype(np.float32)
+        vals[key] = (cur, grad, prev)
+    W, B = D(vals["w"][0]), D(vals["b"][0])
+    dW, dB = D(vals["w"][2]), D(vals["b"][2])
+    S.sgd_update(W, B, D(vals["w"][1]), D(vals["b"][1]), dW, dB, 0.8, 0.0, 0.001, batch, nW, nB)
+    for key, got_v, got_d in (("w", W, dW), ("b", B, dB)):
+        cur, grad, prev = vals[key]
+        deltas = np.float32(0.8) * prev + np.float32(0.001) * grad
+        np.testing.assert_allclose(H(got_v), cur - deltas / np.float32(batch), rtol=1e-6, atol=1e-4)
+        np.testing.assert_allclose(H(got_d), deltas, rtol=1e-6, atol=1e-4)
+
+
+def test_update_parameters_weight_decay(S):
+    rng = np.random.default_rng(5)
+    nW, nB = 777, 13
+    W0, B0 = rng.standard_normal(nW).astype(np.float32), rng.standard_normal(nB).astype(np.float32)
+    gW0, gB0 = rng.standard_normal(nW).astype(np.float32), rng.standard_normal(nB).astype(np.float32)
+    dW0, dB0 = rng.standard_normal(nW).astype(np.float32), rng.standard_normal(nB).astype(np.float32)
+    rW, rB, rdW, rdB = orc.sgd_update(W0, B0, gW0, gB0, dW0, dB0, 0.9, 1e-3, 1e-4, 37)
+    W, B, dW, dB = D(W0), D(B0), D(dW0), D(dB0)
+    S.sgd_update(W, B, D(gW0), D(gB0), dW, dB, 0.9, 1e-3, 1e-4, 37, nW, nB)
+    for got, ref in ((W, rW), (B, rB), (dW, rdW), (dB, rdB)):
+        np.testing.assert_allclose(H(got), ref, rtol=2e-7, atol=1e-7)
+
+
+def test_last_layer_delta_spec(S):
+    rng = np.random.default_rng(7)
+    aw = ah = 6
+    pad = 4
+    gw, gh = aw + 2 * pad, ah + 2 * pad
+    gt = np.full((gh, gw), 99999.0, np.float32)
+    t = (rng.integers(0, 256, (ah, aw)) / 100.0).astype(np.float32)
+    x = (rng.integers(0, 2560, (ah, aw)) / 1000.0).astype(np.float32) - np.float32(1.28)
+    y = np.maximum(x, 0)
+    gt[pad:pad + ah, pad:pad + aw] = t
+    exp = (y - t) * (x > 0)
+    out = zeros(aw * ah)
+    S.last_delta(D(gt), D(y), out, gw, gh, aw, ah, 1)
+    np.testing.assert_array_equal(H(out), exp.ravel())
+
+
+def test_squared_error_spec(S):
+    rng = np.random.default_rng(3)
+    aw, ah, pad = 1000, 2000, 4
+    gw, gh = aw + 2 * pad, ah + 2 * pad
+    gt = np.full((gh, gw), 99999.0, np.float32)
+    gt[pad:pad + ah, pad:pad + aw] = rng.integers(0, 256, (ah, aw))
+    algo = (rng.integers(0, 2560, (ah, aw)) / 10.0).astype(np.float32)
+    d = gt[pad:pad + ah, pad:pad + aw].astype(np.float64) - algo
+    expected = float(np.sum(d * d))
+    nb = S.reduce_workspace_bytes(aw * ah)
+    ws, res = zeros(nb // 4 + 1), zeros(1)
+    S.sq_err(D(gt), D(algo), res, gw, gh, aw, ah, 1, ws, nb)
+    assert abs(float(H(res)[0]) - expected) <= 1e-5 * expected
+
+
+@pytest.mark.parametrize("squared", [False, True])
+def test_sum_spec(S, squared):
+    data = np.arange(900, dtype=np.float32)
+    expected = sum(i * i if squared else i for i in range(900))
+    nb = S.reduce_workspace_bytes(900)
+    ws, res = zeros(nb // 4 + 1), zeros(1)
+    S.buf_sum(D(data), 900, squared, res, ws, nb)
+    assert abs(float(H(res)[0]) - expected) <= 20  # SumTest.cpp:134
+
+
+def test_subtract_from_all_and_mean(S):
+    data = np.arange(900, dtype=np.float32)
+    t = D(data)
+    S.sub_scalar(t, 450.0, 900)
+    np.testing.assert_array_equal(H(t), data - 450.0)
+    t = D(data)
+    nb = S.reduce_workspace_bytes(900)
+    ws, mean = zeros(nb // 4 + 1), zeros(1)
+    S.sub_mean(t, 900, mean, ws, nb)
+    assert float(H(mean)[0]) == pytest.approx(449.5, abs=1e-3)
+    np.testing.assert_allclose(H(t), data - np.float32(449.5), atol=1e-3)
+
+
+@pytest.mark.parametrize("normalize", [True, False])
+def test_extract_luma_spec(S, normalize):
+    d = load("extract_luma.json")
+    rgba = np.array(d["rgba"], np.uint8)
+    out = zeros(d["w"] * d["h"])
+    S.extract_luma(D(rgba, np.uint8), out, d["w"], d["h"], normalize)
+    ref = orc.extract_luma(rgba, d["w"], d["h"], normalize)
+    np.testing.assert_allclose(H(out), ref, rtol=1e-6, atol=1e-6)
+    exp = np.array(d["expected_normalized"], np.float32) * (1 if normalize else 255)
+    np.testing.assert_allclose(H(out), exp, rtol=0, atol=5e-3 * (1 if normalize else 255))
+
+
+def test_swap_luma_spec(S):
+    d = load("swap_luma.json")
+    w, h, pad = d["w"], d["h"], d["padding"]
+    lw, lh = w - 2 * pad, h - 2 * pad
+    n = lw * lw
+    new_luma = (np.arange(n, dtype=np.float32) * np.float32(1.0)) / np.float32(n)
+    rgba = np.array(d["rgba"], np.uint8)
+    out = zeros(w * h * 3, torch.uint8)
+    S.swap_luma(D(rgba, np.uint8), D(new_luma), out, w, h, lw, lh)
+    np.testing.assert_array_equal(H(out), orc.swap_luma(rgba, new_luma, w, h, lw, lh))
+
+
+# ----------------------------------------------------------------------------
+# random shapes vs the oracle (including the SRCNN default / wide layers)
+# ----------------------------------------------------------------------------
+FWD_SHAPES = [
+    # (n_prev, n_cur, f, in_w, in_h, batch, relu)
+    (1, 64, 9, 33, 33, 5, 1),     # default L1
+    (64, 32, 1, 25, 25, 5, 1),    # default L2
+    (32, 1, 5, 25, 25, 5, 0),     # default L3 (SKIP_RELU)
+    (1, 128, 9, 33, 33, 2, 1),    # wide L1
+    (128, 64, 5, 25, 25, 2, 1),   # wide L2
+    (64, 1, 5, 21, 21, 2, 0),     # wide L3
+    (3, 7, 3, 11, 9, 3, 1),       # ragged
+    (1, 1, 1, 1, 1, 1, 0),        # minimal
+    (1, 64, 9, 40, 37, 3, 1),     # non-square, not a 33 tile
+]
+
+
+@pytest.mark.parametrize("shape", FWD_SHAPES, ids=lambda s: "k%d_n%d_f%d_%dx%d_b%d" % s[:6])
+def test_conv_fwd_vs_oracle(S, path, shape):
+    n_prev, n_cur, f, iw, ih, b, relu = shape
+    rng = np.random.default_rng(hash(shape) & 0xFFFF)
+    x = rng.standard_normal(b * iw * ih * n_prev).astype(np.float32)
+    W = (rng.standard_normal(f * f * n_prev * n_cur) / np.sqrt(f * f * n_prev)).astype(np.float32)
+    B = (0.1 * rng.standard_normal(n_cur)).astype(np.float32)
+    ref = orc.conv_fwd(x, W, B, iw, ih, n_prev, n_cur, f, relu, b)
+    out = zeros(ref.size)
+    S.conv_fwd(D(x), out, D(W), D(B), iw, ih, n_prev, n_cur, f, relu, b)
+    assert_close(H(out), ref, RTOL, "conv_fwd")
+
+
+DELTA_SHAPES = [
+    # (n_curr, n_next, f_next, curr_w, curr_h, batch)
+    (32, 1, 5, 25, 25, 4),    # default delta2 (through W3)
+    (64, 32, 1, 25, 25, 4),   # default delta1 (through W2)
+    (64, 1, 5, 21, 21, 2),    # wide delta2
+    (128, 64, 5, 25, 25, 2),  # wide delta1
+    (2, 3, 3, 5, 5, 1),       # LayerDeltasTest shape
+    (5, 4, 3, 9, 7, 3),       # ragged
+]
+
+
+@pytest.mark.parametrize("shape", DELTA_SHAPES, ids=lambda s: "n%d_k%d_f%d_%dx%d_b%d" % s)
+def test_conv_delta_vs_oracle(S, path, shape):
+    n_curr, n_next, f, cw, ch, b = shape
+    rng = np.random.default_rng(hash(shape) & 0xFFFF)
+    nw, nh = cw - f + 1, ch - f + 1
+    d_next = rng.standard_normal(b * nw * nh * n_next).astype(np.float32)
+    y = np.maximum(rng.standard_normal(b * cw * ch * n_curr), 0).astype(np.float32)
+    W = rng.standard_normal(f * f * n_curr * n_next).astype(np.float32)
+    ref = orc.conv_delta(d_next, y, W, f, n_curr, n_next, cw, ch, b)
+    out = zeros(ref.size)
+    S.conv_delta(D(d_next), D(y), out, D(W), f, n_curr, n_next, cw, ch, b)
+    assert_close(H(out), ref, RTOL, "conv_delta")
+
+
+GRAD_SHAPES = [
+    # (n_prev, n_cur, f, out_w, out_h, batch)
+    (1, 64, 9, 25, 25, 6),    # default gW1
+    (64, 32, 1, 25, 25, 6),   # default gW2
+    (32, 1, 5, 21, 21, 6),    # default gW3
+    (128, 64, 5, 21, 21, 2),  # wide gW2
+    (3, 5, 3, 7, 6, 3),       # ragged
+]
+
+
+@pytest.mark.parametrize("shape", GRAD_SHAPES, ids=lambda s: "k%d_n%d_f%d_%dx%d_b%d" % s)
+def test_conv_grad_vs_oracle(S, path, shape):
+    n_prev, n_cur, f, ow, oh, b = shape
+    rng = np.random.default_rng(hash(shape) & 0xFFFF)
+    iw, ih = ow + f - 1, oh + f - 1
+    inp = rng.standard_normal(b * iw * ih * n_prev).astype(np.float32)
+    dl = rng.standard_normal(b * ow * oh * n_cur).astype(np.float32)
+    gW0 = rng.standard_normal(f * f * n_prev * n_cur).astype(np.float32)
+    gB0 = rng.standard_normal(n_cur).astype(np.float32)
+    rW, rB = orc.conv_grad_acc(inp, dl, gW0, gB0, n_prev, n_cur, f, ow, oh, b)
+    nbytes = S.conv_grad_workspace_bytes(n_prev, n_cur, f, ow, oh, b)
+    ws = zeros(nbytes // 4 + 1)
+    gW, gB = D(gW0), D(gB0)
+    S.conv_grad_acc(D(inp), D(dl), gW, gB, n_prev, n_cur, f, ow, oh, b, ws, nbytes)
+    assert_close(H(gW), rW, RTOL, "gW")
+    assert_close(H(gB), rB, RTOL, "gB")
+
+
+# ----------------------------------------------------------------------------
+# network level (ConfigBasedDataPipeline) vs the oracle
+# ----------------------------------------------------------------------------
+NETS = {"default": (64, 32, 9, 1, 5), "wide": (128, 64, 9, 5, 5), "tiny": (8, 4, 5, 1, 3)}
+
+
+@pytest.mark.parametrize("name,batch,size", [("default", 16, 33), ("wide", 3, 33), ("tiny", 5, 15),
+                                             ("default", 2, 48)])
+def test_train_step_vs_oracle(S, path, name, batch, size):
+    cfg = NETS[name]
+    net = S.Net(*cfg)
+    rng = np.random.default_rng(42)
+    X, T = make_batch(rng, batch, size, size)
+    params = make_params(rng, cfg, sd=0.05)
+    P = params.size
+    g0 = (1e-3 * rng.standard_normal(P)).astype(np.float32)
+    rg, acts = orc.train_fwd_bwd(cfg, X, T, size, size, batch, params, g0)
+    nbytes = S.train_workspace_bytes(net, size, size, batch)
+    ws = torch.empty(nbytes // 4 + 64, dtype=torch.float32, device="cuda")
+    g = D(g0)
+    err = zeros(1)
+    S.train_fwd_bwd(net, D(X), D(T), size, size, batch, D(params), g, err, ws, nbytes)
+    got = H(g)
+    off = S.net_offsets(net) + [P]
+    for i, nm in enumerate(["W1", "B1", "W2", "B2", "W3", "B3"]):
+        assert_close(got[off[i]:off[i + 1]], rg[off[i]:off[i + 1]], RTOL, "grad " + nm)
+    # validation metric over the same forward
+    pad = cfg[2] + cfg[3] + cfg[4] - 3
+    A3 = orc.forward(cfg, X, size, size, batch, params)
+    ref_err = orc.sq_err(T, A3, size, size, size - pad, size - pad, batch)
+    assert float(H(err)[0]) == pytest.approx(ref_err, rel=1e-4)
+    # update
+    mom0 = (1e-3 * rng.standard_normal(P)).astype(np.float32)
+    lr = [1e-4, 1e-4, 1e-5]
+    rp, rg2, rm = orc.update_all(cfg, params, rg, mom0, 0.9, 1e-3, lr, batch)
+    p_dev, m_dev = D(params), D(mom0)
+    g_ref_dev = D(rg)  # update from identical grads -> isolates the update kernel
+    S.update_all(net, p_dev, g_ref_dev, m_dev, 0.9, 1e-3, lr, batch)
+    np.testing.assert_allclose(H(p_dev), rp, rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(H(m_dev), rm, rtol=1e-6, atol=1e-9)
+    assert not H(g_ref_dev).any()
+
+
+def test_forward_vs_oracle(S, path):
+    cfg = NETS["default"]
+    net = S.Net(*cfg)
+    rng = np.random.default_rng(9)
+    w, h, b = 256, 256, 1   # BASELINE config 1: one 256x256 tile
+    X, _ = make_batch(rng, b, w, h)
+    params = make_params(rng, cfg, sd=0.05)
+    ref = orc.forward(cfg, X, w, h, b, params)
+    nbytes = S.forward_workspace_bytes(net, w, h, b)
+    ws = torch.empty(nbytes // 4 + 64, dtype=torch.float32, device="cuda")
+    out = zeros(ref.size)
+    S.forward(net, D(X), w, h, b, D(params), out, ws, nbytes)
+    assert_close(H(out), ref, RTOL, "forward 256x256")
+
+
+# ----------------------------------------------------------------------------
+# full size (BASELINE config 2: default net, 33x33, batch 4096)
+# ----------------------------------------------------------------------------
+def test_full_batch_gradients_vs_oracle(S):
+    cfg = NETS["default"]
+    net = S.Net(*cfg)
+    batch, size = 4096, 33
+    rng = np.random.default_rng(2024)
+    X, T = make_batch(rng, batch, size, size)
+    params = make_params(rng, cfg, sd=0.05)
+    P = params.size
+    rg, _ = orc.train_fwd_bwd(cfg, X, T, size, size, batch, params, np.zeros(P, np.float32))
+    nbytes = S.train_workspace_bytes(net, size, size, batch)
+    ws = torch.empty(nbytes // 4 + 64, dtype=torch.float32, device="cuda")
+    Xd, Td, pd = D(X), D(T), D(params)
+    g = zeros(P)
+    S.train_fwd_bwd(net, Xd, Td, size, size, batch, pd, g, None, ws, nbytes)
+    got = H(g)
+    off = S.net_offsets(net) + [P]
+    for i, nm in enumerate(["W1", "B1", "W2", "B2", "W3", "B3"]):
+        assert_close(got[off[i]:off[i + 1]], rg[off[i]:off[i + 1]], RTOL, "full-batch grad " + nm)
+    # determinism: a second pass gives bit-identical gradients
+    g2 = zeros(P)
+    S.train_fwd_bwd(net, Xd, Td, size, size, batch, pd, g2, None, ws, nbytes)
+    np.testing.assert_array_equal(H(g2), got)
+    # chunk linearity: two 2048-tile chunks accumulate to the same gradient
+    g3 = zeros(P)
+    half = batch // 2
+    n = size * size
+    S.train_fwd_bwd(net, Xd[:half * n], Td[:half * n], size, size, half, pd, g3, None, ws, nbytes)
+    S.train_fwd_bwd(net, Xd[half * n:], Td[half * n:], size, size, half, pd, g3, None, ws, nbytes)
+    assert_close(H(g3), got, RTOL, "chunked accumulation")
+
+
+# ----------------------------------------------------------------------------
+# error behaviour (reference: std::runtime_error from the launchers)
+# ----------------------------------------------------------------------------
+def test_invalid_arguments_raise(S):
+    with pytest.raises(S.SrcnnError) as e:
+        S.conv_fwd(zeros(1), zeros(1), zeros(1), zeros(1), 3, 3, 1, 1, 5, 1, 1)  # f > input
+    assert e.value.code == S.ERR_INVALID
+    with pytest.raises(S.SrcnnError) as e:
+        S.conv_grad_acc(zeros(81), zeros(81), zeros(81), zeros(1), 1, 1, 1, 9, 9, 1, zeros(1), 0)
+    assert e.value.code in (S.ERR_WORKSPACE, S.ERR_INVALID)
+    with pytest.raises(S.SrcnnError) as e:
+        S.train_fwd_bwd(S.Net(64, 32, 9, 2, 5), zeros(1), zeros(1), 33, 33, 1, zeros(1), zeros(1),
+                        None, zeros(1), 4)
+    assert e.value.code == S.ERR_INVALID   # even f2 (Config.cpp:64-66)
