@@ -237,6 +237,12 @@ size_t srcnn_train_workspace_bytes(const srcnn_net* net, uint32_t w, uint32_t h,
                        grad_ws_bytes(net->n1, net->n2, net->f2, d.w2, d.h2, batch),
                        grad_ws_bytes(net->n2, 1, net->f3, d.w3, d.h3, batch),
                        srcnn_reduce_workspace_bytes(d.s3 * batch)});
+  size_t fused_need = 0;
+  if (fast_enabled() &&
+      srcnn::fused::train_fwd_bwd(net, nullptr, nullptr, w, h, batch, nullptr, nullptr, nullptr,
+                                  nullptr, nullptr, nullptr, nullptr, 0, nullptr, true,
+                                  &fused_need) == 1)
+    g = std::max(g, fused_need);
   return b + align_up(g);
 }
 
@@ -272,6 +278,12 @@ int srcnn_train_fwd_bwd(const srcnn_net* net, const float* X, const float* T, ui
   float *gW1 = grads + off[0], *gB1 = grads + off[1], *gW2 = grads + off[2],
         *gB2 = grads + off[3], *gW3 = grads + off[4], *gB3 = grads + off[5];
   int rc;
+  if (fast_enabled()) {
+    rc = srcnn::fused::train_fwd_bwd(net, X, T, w, h, batch, params, grads, sq_err, A1, A2, D2,
+                                     static_cast<float*>(gws), gws_bytes, srcnn::as_stream(stream),
+                                     false, nullptr);
+    if (rc != 0) return rc < 0 ? rc : SRCNN_OK;
+  }
   // forward: ConfigBasedDataPipeline.cpp:375-397
   if ((rc = srcnn_conv_fwd(X, A1, W1, B1, w, h, 1, net->n1, net->f1, 1, batch, stream))) return rc;
   if ((rc = srcnn_conv_fwd(A1, A2, W2, B2, d.w1, d.h1, net->n1, net->n2, net->f2, 1, batch, stream)))

@@ -38,6 +38,16 @@ int try_conv_grad_acc(const float* in, const float* d, float* gW, float* gB, uin
                       uint32_t batch, void* ws, size_t ws_bytes, hipStream_t s);
 }  // namespace fast
 
+// Fused training step for nets with a 1x1 middle layer (train_fused.hip).
+// Returns 1 when the net/shape is specialised (step enqueued, or with
+// query_only the slab workspace size written to *need), 0 when not.
+namespace fused {
+int train_fwd_bwd(const srcnn_net* net, const float* X, const float* T, uint32_t w, uint32_t h,
+                  uint32_t batch, const float* params, float* grads, float* sq_err, float* A1,
+                  float* A2, float* D2, float* slab, size_t slab_bytes, hipStream_t s,
+                  bool query_only, size_t* need);
+}  // namespace fused
+
 int sgd_update(float* W, float* B, const float* gW, const float* gB, float* dW, float* dB,
                float mu, float wd, float lr, uint32_t batch, uint32_t nW, uint32_t nB,
                hipStream_t s);

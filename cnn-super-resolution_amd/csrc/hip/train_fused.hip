@@ -1,0 +1,722 @@
+// train_fused.hip -- gfx950 fused training step for SRCNN nets with a 1x1
+// middle layer (f2 == 1), e.g. the reference default n1=64, n2=32, f1=9, f3=5.
+//
+// The reference runs one OpenCL kernel per op (ConfigBasedDataPipeline.cpp:
+// 359-482): 3 forward, last delta, 2 deltas, 3 gradient kernels, every tensor
+// round-tripping through global memory and the gradients summed serially per
+// weight (backpropagate.cl:89-106).  Here the same mathematics runs as three
+// kernels plus a deterministic reduction:
+//
+//   l12_fwd      L1 (f1 x f1 x 1 -> n1) and L2 (1x1, n1 -> n2) as fp32 MFMA
+//                implicit GEMMs per 32-pixel chunk; A1 goes to HBM (needed by
+//                backward) and through a per-wave LDS transpose into L2.
+//   l3_delta     per sample: A2 tile in LDS; L3 (f3 x f3 x n2 -> 1, VALU),
+//                last-layer delta with the reference quirk, delta2 (MFMA over
+//                the 25 taps), gW3 (MFMA over pixels), gB3, squared error.
+//   d1_grad12    delta1 = relu'(A1) * (delta2 . W2^T) (MFMA), then gW2 and gW1
+//                consume delta1 / A1 straight from the accumulator registers
+//                (mfma.hpp: k-slot <-> pixel pairing), gB1 via a ones row.
+//   slab_reduce  per-block partial gradients summed in block order -> grads.
+//
+// HBM traffic per 33x33 tile: X 4.4 KB + A1 160 KB (write + read) + A2 80 KB
+// (write + read) + delta2 80 KB (write + read) ~ 650 KB vs 1.54 MB for the
+// layer-by-layer dataflow.  Results are deterministic: the
+// sample -> block -> wave assignment is static and every sum has a fixed
+// order; no float atomics anywhere.
+#include "common.hpp"
+#include "mfma.hpp"
+#include "ops.hpp"
+
+namespace srcnn {
+namespace fused {
+
+using mfma::crow;
+using mfma::f32x16;
+using mfma::mma;
+using mfma::zero16;
+
+constexpr int kXsMax = 2048;  // input sample / region tile (floats) staged in LDS
+
+struct Geom {
+  int W, H;      // input sample
+  int ow, oh;    // L1 (and L2) output
+  int rw, rh;    // region of L1 output handled per work item
+  int nrx, nry;  // regions per sample
+  int batch;
+};
+
+// ---------------------------------------------------------------------------
+// Kernel 1: L1 (+ L2) forward
+// ---------------------------------------------------------------------------
+template <int N1, int N2, int F1, bool STORE_A1, bool DO_L2>
+__global__ __launch_bounds__(256, 2) void l12_fwd_kernel(
+    const float* __restrict__ X, const float* __restrict__ W1, const float* __restrict__ B1,
+    const float* __restrict__ W2, const float* __restrict__ B2, float* __restrict__ A1,
+    float* __restrict__ A2, Geom g) {
+  constexpr int K1 = F1 * F1, KS1 = (K1 + 1) / 2, NT1 = N1 / 32;
+  constexpr int NT2 = (N2 + 31) / 32, KS2 = N1 / 2;
+  constexpr int TS = N1 + 1;  // padded row of the per-wave A1 transpose
+  __shared__ float xs[kXsMax];
+  __shared__ float ts[DO_L2 ? 4 : 1][32][DO_L2 ? TS : 1];
+  __shared__ int gidx[4][32];
+
+  const int lane = mfma::lane_id(), wave = mfma::wave_id();
+  const int h = lane >> 5, li = lane & 31;
+  const int tw = g.rw + F1 - 1;  // LDS row stride of the input tile
+
+  // B operands of L1: W1[tap = 2s + h][n = 32t + li]
+  float w1f[KS1][NT1];
+#pragma unroll
+  for (int s = 0; s < KS1; s++)
+#pragma unroll
+    for (int t = 0; t < NT1; t++) {
+      const int tap = 2 * s + h;
+      w1f[s][t] = tap < K1 ? W1[tap * N1 + 32 * t + li] : 0.0f;
+    }
+  float b1v[NT1];
+#pragma unroll
+  for (int t = 0; t < NT1; t++) b1v[t] = B1[32 * t + li];
+  // B operands of L2: W2[c = 2s + h][n = 32u + li]
+  float w2f[DO_L2 ? KS2 : 1][NT2];
+  float b2v[NT2];
+  if constexpr (DO_L2) {
+#pragma unroll
+    for (int s = 0; s < KS2; s++)
+#pragma unroll
+      for (int u = 0; u < NT2; u++) {
+        const int n = 32 * u + li;
+        w2f[s][u] = n < N2 ? W2[(2 * s + h) * N2 + n] : 0.0f;
+      }
+#pragma unroll
+    for (int u = 0; u < NT2; u++) b2v[u] = (32 * u + li) < N2 ? B2[32 * u + li] : 0.0f;
+  }
+
+  const int per_sample = g.nry * g.nrx;
+  const int n_items = g.batch * per_sample;
+  for (int wi = blockIdx.x; wi < n_items; wi += gridDim.x) {
+    const int sample = wi / per_sample;
+    const int rr = wi - sample * per_sample;
+    const int ry = rr / g.nrx, rx = rr - ry * g.nrx;
+    const int oy0 = ry * g.rh, ox0 = rx * g.rw;
+    const int crh = min(g.rh, g.oh - oy0), crw = min(g.rw, g.ow - ox0);
+    const int th = crh + F1 - 1, tww = crw + F1 - 1;
+
+    __syncthreads();  // previous work item's readers are done with xs
+    const float* xsrc = X + (size_t)sample * g.W * g.H + (size_t)oy0 * g.W + ox0;
+    for (int i = threadIdx.x; i < th * tww; i += blockDim.x) {
+      const int iy = i / tww, ix = i - iy * tww;
+      xs[iy * tw + ix] = xsrc[(size_t)iy * g.W + ix];
+    }
+    __syncthreads();
+
+    const int npx = crh * crw;
+    const int nch = (npx + 31) / 32;
+    for (int c = wave; c < nch; c += 4) {
+      // this lane's own pixel (A-operand row li)
+      const int p = c * 32 + li;
+      const bool valid = p < npx;
+      const int pc = valid ? p : npx - 1;
+      const int iy = pc / crw, ix = pc - iy * crw;
+      const int xb = iy * tw + ix;
+      if (h == 0)
+        gidx[wave][li] = valid ? (sample * g.oh + oy0 + iy) * g.ow + ox0 + ix : -1;
+
+      f32x16 acc1[NT1];
+#pragma unroll
+      for (int t = 0; t < NT1; t++) acc1[t] = zero16();
+#pragma unroll
+      for (int s = 0; s < KS1; s++) {
+        constexpr int dummy = 0;
+        (void)dummy;
+        const int k0 = 2 * s, k1 = 2 * s + 1;
+        const int o0 = (k0 / F1) * tw + (k0 % F1);
+        const int o1 = k1 < K1 ? (k1 / F1) * tw + (k1 % F1) : 0;
+        const float a = xs[xb + (h ? o1 : o0)];
+#pragma unroll
+        for (int t = 0; t < NT1; t++) acc1[t] = mma(a, w1f[s][t], acc1[t]);
+      }
+
+      // epilogue L1: bias + ReLU (layer_uber_kernel.cl:88-95), store A1 (HWC)
+#pragma unroll
+      for (int r = 0; r < 16; r++) {
+        const int gp = gidx[wave][crow(r, h)];
+#pragma unroll
+        for (int t = 0; t < NT1; t++) {
+          const float v = fmaxf(acc1[t][r] + b1v[t], 0.0f);
+          if constexpr (STORE_A1) {
+            if (gp >= 0) A1[(size_t)gp * N1 + 32 * t + li] = v;
+          }
+          if constexpr (DO_L2) ts[wave][crow(r, h)][32 * t + li] = v;
+        }
+      }
+      if constexpr (DO_L2) {
+        __builtin_amdgcn_wave_barrier();
+        f32x16 acc2[NT2];
+#pragma unroll
+        for (int u = 0; u < NT2; u++) acc2[u] = zero16();
+#pragma unroll
+        for (int s = 0; s < KS2; s++) {
+          const float a = ts[wave][li][2 * s + h];  // A1[pixel li][channel 2s+h]
+#pragma unroll
+          for (int u = 0; u < NT2; u++) acc2[u] = mma(a, w2f[s][u], acc2[u]);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+          const int gp = gidx[wave][crow(r, h)];
+#pragma unroll
+          for (int u = 0; u < NT2; u++) {
+            const int n = 32 * u + li;
+            if (gp >= 0 && n < N2) A2[(size_t)gp * N2 + n] = fmaxf(acc2[u][r] + b2v[u], 0.0f);
+          }
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Kernel 2: L3 forward + last-layer delta + delta2 + gW3/gB3 (+ squared error)
+// one sample per iteration, 8 waves, A2 tile resident in LDS
+// ---------------------------------------------------------------------------
+struct L3Geom {
+  int W, H;     // ground-truth sample (= network input size)
+  int w2, h2;   // A2
+  int w3, h3;   // A3
+  int batch;
+};
+
+template <int N2, int F3>
+__global__ __launch_bounds__(512, 1) void l3_delta_kernel(
+    const float* __restrict__ A2, const float* __restrict__ T, const float* __restrict__ W3,
+    const float* __restrict__ B3, float* __restrict__ D2, float* __restrict__ slab3,
+    float* __restrict__ sq_slab, L3Geom g) {
+  constexpr int K3 = F3 * F3, KS3 = (K3 + 1) / 2, NT2 = (N2 + 31) / 32;
+  constexpr int N2S = N2 + 4;      // padded A2 row: conflict-free ds_read_b128
+  constexpr int NW3 = K3 * N2;     // gW3 size; slab row = NW3 + 1 (gB3)
+  static_assert(K3 <= 32, "taps must fit one 32-row MFMA tile");
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int npx2 = g.w2 * g.h2, npx3 = g.w3 * g.h3;
+  const int w3p = g.w3 + 2 * (F3 - 1), h3p = g.h3 + 2 * (F3 - 1);
+  float* a2s = smem;                                   // [npx2][N2S]
+  float* d3p = smem + ((npx2 * N2S + 3) & ~3);         // [h3p][w3p], zero border
+  float* red = d3p + ((w3p * h3p + 3) & ~3);           // [1024] reduction scratch
+
+  const int lane = mfma::lane_id(), wave = mfma::wave_id();
+  const int h = lane >> 5, li = lane & 31;
+  const int nwaves = blockDim.x >> 6;
+  const int pad = (g.W - g.w3) / 2;  // last_layer_delta.cl:25
+
+  for (int i = threadIdx.x; i < w3p * h3p; i += blockDim.x) d3p[i] = 0.0f;
+
+  // delta2 B operands: W3[tap = 2s + h][n = 32u + li]
+  float w3f[KS3][NT2];
+#pragma unroll
+  for (int s = 0; s < KS3; s++)
+#pragma unroll
+    for (int u = 0; u < NT2; u++) {
+      const int tap = 2 * s + h, n = 32 * u + li;
+      w3f[s][u] = (tap < K3 && n < N2) ? W3[tap * N2 + n] : 0.0f;
+    }
+  // gW3 A-operand row of this lane: tap li
+  const int my_dy = li / F3, my_dx = li - (li / F3) * F3;
+  const bool my_tap = li < K3;
+
+  f32x16 gacc[NT2];
+#pragma unroll
+  for (int u = 0; u < NT2; u++) gacc[u] = zero16();
+  float gb3 = 0.0f, sq = 0.0f;
+  const float b3 = B3[0];
+
+  for (int sample = blockIdx.x; sample < g.batch; sample += gridDim.x) {
+    __syncthreads();
+    // A2 sample -> LDS (coalesced float4)
+    const float4* src = reinterpret_cast<const float4*>(A2 + (size_t)sample * npx2 * N2);
+    for (int i = threadIdx.x; i < npx2 * (N2 / 4); i += blockDim.x) {
+      const int p = i / (N2 / 4), q = i - p * (N2 / 4);
+      *reinterpret_cast<float4*>(a2s + p * N2S + 4 * q) = src[i];
+    }
+    __syncthreads();
+
+    // L3 forward (layer_uber_kernel.cl:70-91, SKIP_RELU) + last delta
+    // (last_layer_delta.cl:34-48) + squared error (squared_error.cl:60-69)
+    for (int o = threadIdx.x; o < npx3; o += blockDim.x) {
+      const int y = o / g.w3, x = o - y * g.w3;
+      float acc0 = 0.f, acc1 = 0.f;
+#pragma unroll
+      for (int dy = 0; dy < F3; dy++)
+#pragma unroll
+        for (int dx = 0; dx < F3; dx++) {
+          const float* ap = a2s + ((y + dy) * g.w2 + x + dx) * N2S;
+          const float* wp = W3 + (dy * F3 + dx) * N2;
+#pragma unroll
+          for (int q = 0; q < N2 / 4; q++) {
+            const float4 a = *reinterpret_cast<const float4*>(ap + 4 * q);
+            acc0 += a.x * wp[4 * q + 0];
+            acc1 += a.y * wp[4 * q + 1];
+            acc0 += a.z * wp[4 * q + 2];
+            acc1 += a.w * wp[4 * q + 3];
+          }
+        }
+      const float a3 = (acc0 + acc1) + b3;
+      const float t = T[(size_t)sample * g.W * g.H + (size_t)(y + pad) * g.W + x + pad];
+      const float diff = a3 - t;
+      const float d3 = diff * (a3 > 0.0f ? 1.0f : 0.0f);
+      d3p[(y + F3 - 1) * w3p + x + F3 - 1] = d3;
+      gb3 += d3;
+      sq += diff * diff;
+    }
+    __syncthreads();
+
+    // delta2 (layer_deltas.cl:79-123): per 32-pixel chunk of the A2 grid,
+    // D[pixel][n] = sum_tap d3p[pixel - tap] * W3[tap][n], masked by A2 > 0
+    const int nch = (npx2 + 31) / 32;
+    for (int c = wave; c < nch; c += nwaves) {
+      const int p = min(c * 32 + li, npx2 - 1);
+      const int y = p / g.w2, x = p - y * g.w2;
+      const int base = (y + F3 - 1) * w3p + x + F3 - 1;
+      f32x16 acc[NT2];
+#pragma unroll
+      for (int u = 0; u < NT2; u++) acc[u] = zero16();
+#pragma unroll
+      for (int s = 0; s < KS3; s++) {
+        const int k0 = 2 * s, k1 = 2 * s + 1;
+        const int o0 = (k0 / F3) * w3p + (k0 % F3);
+        const int o1 = k1 < K3 ? (k1 / F3) * w3p + (k1 % F3) : 0;
+        const float a = d3p[base - (h ? o1 : o0)];
+#pragma unroll
+        for (int u = 0; u < NT2; u++) acc[u] = mma(a, w3f[s][u], acc[u]);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; r++) {
+        const int pr = c * 32 + crow(r, h);
+        if (pr < npx2) {
+#pragma unroll
+          for (int u = 0; u < NT2; u++) {
+            const int n = 32 * u + li;
+            if (n < N2) {
+              const float m = a2s[pr * N2S + n] > 0.0f ? 1.0f : 0.0f;
+              D2[((size_t)sample * npx2 + pr) * N2 + n] = acc[u][r] * m;
+            }
+          }
+        }
+      }
+    }
+
+    // gW3 (backpropagate.cl:89-106): G[tap][n] += sum_p' d3p[p' - tap] * A2[p'][n]
+    {
+      const int nks = (npx2 + 1) / 2;
+      int pp = 2 * wave + h;  // p' of this lane for k-step `wave`
+      int yq = pp / g.w2, xq = pp - yq * g.w2;
+      const int stride = 2 * nwaves;
+      for (int j = wave; j < nks; j += nwaves) {
+        const bool v = pp < npx2;
+        const float a = (v && my_tap) ? d3p[(yq - my_dy + F3 - 1) * w3p + xq - my_dx + F3 - 1] : 0.0f;
+#pragma unroll
+        for (int u = 0; u < NT2; u++) {
+          const int n = 32 * u + li;
+          const float b = (v && n < N2) ? a2s[pp * N2S + n] : 0.0f;
+          gacc[u] = mma(a, b, gacc[u]);
+        }
+        pp += stride;
+        xq += stride;
+        while (xq >= g.w2) {
+          xq -= g.w2;
+          yq++;
+        }
+      }
+    }
+  }
+
+  // ---- block reduction of the partial gradients, in wave order ----
+  __syncthreads();
+  for (int w = 0; w < nwaves; w++) {
+    if (wave == w) {
+#pragma unroll
+      for (int u = 0; u < NT2; u++)
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+          float* dst = red + (u * 16 + r) * 64 + lane;
+          *dst = (w == 0 ? 0.0f : *dst) + gacc[u][r];
+        }
+    }
+    __syncthreads();
+  }
+  float* out = slab3 + (size_t)blockIdx.x * (NW3 + 1);
+  for (int i = threadIdx.x; i < NT2 * 16 * 64; i += blockDim.x) {
+    const int u = i / 1024, r = (i >> 6) & 15, l = i & 63;
+    const int tap = crow(r, l >> 5), n = 32 * u + (l & 31);
+    if (tap < K3 && n < N2) out[tap * N2 + n] = red[i];
+  }
+  // gB3 and squared error: per-wave shuffle trees, then waves in order
+  for (int off = 32; off > 0; off >>= 1) {
+    gb3 += __shfl_down(gb3, off, 64);
+    sq += __shfl_down(sq, off, 64);
+  }
+  __syncthreads();
+  if (lane == 0) {
+    red[2 * wave] = gb3;
+    red[2 * wave + 1] = sq;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float tb = 0.f, ts = 0.f;
+    for (int w = 0; w < nwaves; w++) {
+      tb += red[2 * w];
+      ts += red[2 * w + 1];
+    }
+    out[NW3] = tb;
+    sq_slab[blockIdx.x] = ts;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Kernel 3: delta1 + gW2/gB2 + gW1/gB1
+// ---------------------------------------------------------------------------
+template <int N1, int N2, int F1>
+__global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
+    const float* __restrict__ X, const float* __restrict__ A1, const float* __restrict__ D2,
+    const float* __restrict__ W2, float* __restrict__ slab, Geom g) {
+  constexpr int K1 = F1 * F1, NT1 = N1 / 32, NT2 = (N2 + 31) / 32;
+  constexpr int MT = (K1 + 1 + 31) / 32;  // tap tiles (+1 ones row -> gB1)
+  constexpr int KD = (N2 + 1) / 2;        // delta1 k-steps (over n)
+  constexpr int DS = N2 + 1;              // padded delta2 row in LDS
+  constexpr int WS = N2 + 1;              // padded W2 row in LDS
+  constexpr int NW1 = K1 * N1, NW2 = N1 * N2;
+  constexpr int P12 = NW1 + N1 + NW2 + N2;  // [gW1 | gB1 | gW2 | gB2]
+  constexpr int RED = (MT * NT1 + NT1 * NT2) * 16 * 64;
+  static_assert(N2 % 2 == 0, "n2 must be even");
+  constexpr int LDS_MAIN = kXsMax + N1 * WS + 4 * 32 * DS;
+  constexpr int LDS_TOTAL = LDS_MAIN > RED ? LDS_MAIN : RED;
+  __shared__ __attribute__((aligned(16))) float smem[LDS_TOTAL];
+  __shared__ int xbt[4][32];
+  float* xs = smem;
+  float* w2s = smem + kXsMax;          // [N1][WS]: W2[c][n]
+  float* d2w = w2s + N1 * WS;          // [4][32][DS]
+
+  const int lane = mfma::lane_id(), wave = mfma::wave_id();
+  const int h = lane >> 5, li = lane & 31;
+  const int npx = g.ow * g.oh;
+
+  for (int i = threadIdx.x; i < N1 * N2; i += blockDim.x) {
+    const int c = i / N2, n = i - c * N2;
+    w2s[c * WS + n] = W2[i];
+  }
+  // gW1 A-operand rows of this lane: taps 32m + li (tap K1 = ones -> gB1)
+  int toff[MT];
+  float tsel[MT];  // 0: zero row, 1: X tap, 2: ones row
+#pragma unroll
+  for (int m = 0; m < MT; m++) {
+    const int tap = 32 * m + li;
+    toff[m] = tap < K1 ? (tap / F1) * g.W + (tap % F1) : 0;
+    tsel[m] = tap < K1 ? 1.0f : (tap == K1 ? 2.0f : 0.0f);
+  }
+
+  f32x16 g1[MT][NT1], g2[NT1][NT2];
+#pragma unroll
+  for (int m = 0; m < MT; m++)
+#pragma unroll
+    for (int t = 0; t < NT1; t++) g1[m][t] = zero16();
+#pragma unroll
+  for (int t = 0; t < NT1; t++)
+#pragma unroll
+    for (int u = 0; u < NT2; u++) g2[t][u] = zero16();
+  float gb2[NT2];
+#pragma unroll
+  for (int u = 0; u < NT2; u++) gb2[u] = 0.0f;
+
+  float* d2me = d2w + wave * 32 * DS;
+  for (int sample = blockIdx.x; sample < g.batch; sample += gridDim.x) {
+    __syncthreads();
+    const float* xsrc = X + (size_t)sample * g.W * g.H;
+    for (int i = threadIdx.x; i < g.W * g.H; i += blockDim.x) xs[i] = xsrc[i];
+    __syncthreads();
+
+    const int nch = (npx + 31) / 32;
+    for (int c = wave; c < nch; c += 4) {
+      {  // this lane's own pixel -> X base offset table
+        const int p = min(c * 32 + li, npx - 1);
+        const int y = p / g.ow, x = p - y * g.ow;
+        if (h == 0) xbt[wave][li] = y * g.W + x;
+      }
+      // stage the delta2 chunk [32 px][N2] (zero rows past the sample)
+      const float* dsrc = D2 + ((size_t)sample * npx + c * 32) * N2;
+      for (int i = lane; i < 32 * N2 / 4; i += 64) {
+        const int row = i / (N2 / 4), q = i - row * (N2 / 4);
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (c * 32 + row < npx) v = reinterpret_cast<const float4*>(dsrc)[i];
+        float* d = d2me + row * DS + 4 * q;
+        d[0] = v.x;
+        d[1] = v.y;
+        d[2] = v.z;
+        d[3] = v.w;
+      }
+      // A1 in accumulator layout: a1[t][r] = A1[pixel crow(r,h)][32t + li]
+      float a1[NT1][16];
+#pragma unroll
+      for (int r = 0; r < 16; r++) {
+        const int pr = c * 32 + crow(r, h);
+#pragma unroll
+        for (int t = 0; t < NT1; t++)
+          a1[t][r] = pr < npx ? A1[((size_t)sample * npx + pr) * N1 + 32 * t + li] : 0.0f;
+      }
+      __builtin_amdgcn_wave_barrier();
+
+      // delta1[p][c] = [A1 > 0] * sum_n delta2[p][n] * W2[c][n]  (layer_deltas.cl, f=1)
+      f32x16 d1[NT1];
+#pragma unroll
+      for (int t = 0; t < NT1; t++) d1[t] = zero16();
+#pragma unroll
+      for (int s = 0; s < KD; s++) {
+        const int n = 2 * s + h;
+        const float a = n < N2 ? d2me[li * DS + n] : 0.0f;
+#pragma unroll
+        for (int t = 0; t < NT1; t++) {
+          const float b = n < N2 ? w2s[(32 * t + li) * WS + n] : 0.0f;
+          d1[t] = mma(a, b, d1[t]);
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < NT1; t++)
+#pragma unroll
+        for (int r = 0; r < 16; r++) d1[t][r] = a1[t][r] > 0.0f ? d1[t][r] : 0.0f;
+
+      // gW2[c][n] += sum_p A1[p][c] delta2[p][n]; gB2[n] += sum_p delta2[p][n]
+#pragma unroll
+      for (int s = 0; s < 16; s++) {
+        const int pr = crow(s, h);
+#pragma unroll
+        for (int u = 0; u < NT2; u++) {
+          const int n = 32 * u + li;
+          const float b = n < N2 ? d2me[pr * DS + n] : 0.0f;
+          gb2[u] += b;
+#pragma unroll
+          for (int t = 0; t < NT1; t++) g2[t][u] = mma(a1[t][s], b, g2[t][u]);
+        }
+      }
+      // gW1[tap][c] += sum_p X[p + tap] delta1[p][c]; ones row -> gB1[c]
+#pragma unroll
+      for (int s = 0; s < 16; s++) {
+        const int xb = xbt[wave][crow(s, h)];
+#pragma unroll
+        for (int m = 0; m < MT; m++) {
+          const float xv = xs[xb + toff[m]];
+          const float a = tsel[m] == 1.0f ? xv : (tsel[m] == 2.0f ? 1.0f : 0.0f);
+#pragma unroll
+          for (int t = 0; t < NT1; t++) g1[m][t] = mma(a, d1[t][s], g1[m][t]);
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+
+  // ---- block reduction (waves in order) into LDS, then one slab per block ----
+  __syncthreads();
+  float* red = smem;
+  for (int w = 0; w < 4; w++) {
+    if (wave == w) {
+      int k = 0;
+#pragma unroll
+      for (int m = 0; m < MT; m++)
+#pragma unroll
+        for (int t = 0; t < NT1; t++, k++)
+#pragma unroll
+          for (int r = 0; r < 16; r++) {
+            float* d = red + (k * 16 + r) * 64 + lane;
+            *d = (w == 0 ? 0.0f : *d) + g1[m][t][r];
+          }
+#pragma unroll
+      for (int t = 0; t < NT1; t++)
+#pragma unroll
+        for (int u = 0; u < NT2; u++, k++)
+#pragma unroll
+          for (int r = 0; r < 16; r++) {
+            float* d = red + (k * 16 + r) * 64 + lane;
+            *d = (w == 0 ? 0.0f : *d) + g2[t][u][r];
+          }
+    }
+    __syncthreads();
+  }
+  float* out = slab + (size_t)blockIdx.x * P12;
+  for (int i = threadIdx.x; i < RED; i += blockDim.x) {
+    const int k = i / 1024, r = (i >> 6) & 15, l = i & 63;
+    const int row = crow(r, l >> 5), col = l & 31;
+    if (k < MT * NT1) {
+      const int m = k / NT1, t = k - m * NT1;
+      const int tap = 32 * m + row, ch = 32 * t + col;
+      if (tap < K1) out[tap * N1 + ch] = red[i];
+      else if (tap == K1) out[NW1 + ch] = red[i];
+    } else {
+      const int kk = k - MT * NT1;
+      const int t = kk / NT2, u = kk - t * NT2;
+      const int ch = 32 * t + row, n = 32 * u + col;
+      if (n < N2) out[NW1 + N1 + ch * N2 + n] = red[i];
+    }
+  }
+  // gB2: combine the two lane halves, then waves in order
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < NT2; u++) {
+    const float v = gb2[u] + __shfl_down(gb2[u], 32, 64);
+    if (h == 0) red[(wave * NT2 + u) * 32 + li] = v;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < NT2 * 32; i += blockDim.x) {
+    const int u = i / 32, n = 32 * u + (i & 31);
+    if (n < N2) {
+      float v = 0.f;
+      for (int w = 0; w < 4; w++) v += red[(w * NT2 + u) * 32 + (i & 31)];
+      out[NW1 + N1 + NW2 + n] = v;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// deterministic slab reduction: grads[i] += sum_b slab[b][i] (block order)
+// ---------------------------------------------------------------------------
+__global__ void slab_reduce_kernel(const float* __restrict__ slab12, int n12, int P12,
+                                   const float* __restrict__ slab3, int n3, int P3,
+                                   float* __restrict__ grads, const float* __restrict__ sq_slab,
+                                   float* __restrict__ sq_err) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < P12) {
+    float acc = 0.0f;
+    for (int b = 0; b < n12; b++) acc += slab12[(size_t)b * P12 + i];
+    grads[i] += acc;
+  } else if (i < P12 + P3) {
+    const int j = i - P12;
+    float acc = 0.0f;
+    for (int b = 0; b < n3; b++) acc += slab3[(size_t)b * P3 + j];
+    grads[i] += acc;
+  } else if (i == P12 + P3 && sq_err) {
+    float acc = 0.0f;
+    for (int b = 0; b < n3; b++) acc += sq_slab[b];
+    *sq_err += acc;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+struct Plan {
+  int grid12, grid3, grid_d1;
+  size_t l3_lds;
+  size_t slab12_floats, slab3_floats;
+};
+
+template <int N1, int N2, int F1, int F3>
+struct Net {
+  static constexpr int P12 = F1 * F1 * N1 + N1 + N1 * N2 + N2;
+  static constexpr int P3 = F3 * F3 * N2 + 1;
+};
+
+static size_t l3_lds_bytes(int npx2, int n2, int w3p, int h3p) {
+  const size_t a2 = ((size_t)npx2 * (n2 + 4) + 3) & ~size_t(3);
+  const size_t d3 = ((size_t)w3p * h3p + 3) & ~size_t(3);
+  return (a2 + d3 + 1024) * sizeof(float);
+}
+
+static int grid_for_batch(uint32_t batch, int cap) { return (int)std::min<uint32_t>(batch, cap); }
+
+// Returns 1 if the shape is specialised (and the step was enqueued), 0 if
+// not (caller falls back to the op-by-op path), <0 on error.
+template <int N1, int N2, int F1, int F3>
+static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t batch,
+               const float* params, float* grads, float* sq_err, float* A1, float* A2, float* D2,
+               float* slab, size_t slab_bytes, hipStream_t s, bool query_only, size_t* need) {
+  using NetT = Net<N1, N2, F1, F3>;
+  const int ow = w - F1 + 1, oh = h - F1 + 1;
+  const int w3 = ow - F3 + 1, h3 = oh - F3 + 1;
+  if ((int)(w * h) > kXsMax || w3 <= 0 || h3 <= 0) return 0;
+  const size_t lds3 = l3_lds_bytes(ow * oh, N2, w3 + 2 * (F3 - 1), h3 + 2 * (F3 - 1));
+  if (lds3 > 160 * 1024) return 0;
+  const int g12 = grid_for_batch(batch, 1024);
+  const int g3 = grid_for_batch(batch, 256);
+  const int gd = grid_for_batch(batch, 512);
+  const size_t s12 = (size_t)gd * NetT::P12, s3 = (size_t)g3 * NetT::P3;
+  const size_t bytes = (s12 + s3 + g3) * sizeof(float);
+  if (query_only) {
+    *need = bytes;
+    return 1;
+  }
+  if (slab_bytes < bytes)
+    return fail(SRCNN_ERR_WORKSPACE, "fused train step: slab workspace %zu B < %zu B", slab_bytes, bytes);
+  float* slab12 = slab;
+  float* slab3 = slab12 + s12;
+  float* sqs = slab3 + s3;
+  // flat parameter layout [W1|B1|W2|B2|W3|B3]
+  const float* W1 = params;
+  const float* B1 = W1 + F1 * F1 * N1;
+  const float* W2 = B1 + N1;
+  const float* B2 = W2 + N1 * N2;
+  const float* W3 = B2 + N2;
+  const float* B3 = W3 + F3 * F3 * N2;
+  Geom g{(int)w, (int)h, ow, oh, ow, oh, 1, 1, (int)batch};
+  {
+    SRCNN_PROFILE("l12_fwd_mfma", s);
+    hipLaunchKernelGGL((l12_fwd_kernel<N1, N2, F1, true, true>), dim3(g12), dim3(256), 0, s, X, W1,
+                       B1, W2, B2, A1, A2, g);
+    SRCNN_LAUNCH_TRY();
+  }
+  L3Geom lg{(int)w, (int)h, ow, oh, w3, h3, (int)batch};
+  {
+    SRCNN_PROFILE("l3_delta_fused", s);
+    hipLaunchKernelGGL((l3_delta_kernel<N2, F3>), dim3(g3), dim3(512), lds3, s, A2, T, W3, B3, D2,
+                       slab3, sqs, lg);
+    SRCNN_LAUNCH_TRY();
+  }
+  {
+    SRCNN_PROFILE("delta1_grad12_fused", s);
+    hipLaunchKernelGGL((d1_grad12_kernel<N1, N2, F1>), dim3(gd), dim3(256), 0, s, X, A1, D2, W2,
+                       slab12, g);
+    SRCNN_LAUNCH_TRY();
+  }
+  {
+    SRCNN_PROFILE("slab_reduce", s);
+    const int tot = NetT::P12 + NetT::P3 + 1;
+    hipLaunchKernelGGL(slab_reduce_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, slab12, gd,
+                       NetT::P12, slab3, g3, NetT::P3, grads, sqs, sq_err);
+    SRCNN_LAUNCH_TRY();
+  }
+  return 1;
+}
+
+static bool lds_attr_set = false;
+
+template <int N1, int N2, int F1, int F3>
+static int dispatch_one(const srcnn_net* net, const float* X, const float* T, uint32_t w,
+                        uint32_t h, uint32_t batch, const float* params, float* grads,
+                        float* sq_err, float* A1, float* A2, float* D2, float* slab,
+                        size_t slab_bytes, hipStream_t s, bool query_only, size_t* need) {
+  if (net->n1 != (uint32_t)N1 || net->n2 != (uint32_t)N2 || net->f1 != (uint32_t)F1 ||
+      net->f2 != 1 || net->f3 != (uint32_t)F3)
+    return 0;
+  if (!query_only) {
+    // the L3 kernel keeps a whole A2 sample in LDS (> 64 KiB default)
+    hipError_t e = hipFuncSetAttribute((const void*)l3_delta_kernel<N2, F3>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess)
+      return fail(SRCNN_ERR_HIP, "hipFuncSetAttribute(l3_delta): %s", hipGetErrorString(e));
+  }
+  return run<N1, N2, F1, F3>(X, T, w, h, batch, params, grads, sq_err, A1, A2, D2, slab,
+                             slab_bytes, s, query_only, need);
+}
+
+int train_fwd_bwd(const srcnn_net* net, const float* X, const float* T, uint32_t w, uint32_t h,
+                  uint32_t batch, const float* params, float* grads, float* sq_err, float* A1,
+                  float* A2, float* D2, float* slab, size_t slab_bytes, hipStream_t s,
+                  bool query_only, size_t* need) {
+  int rc;
+#define SRCNN_FUSED_CASE(n1, n2, f1, f3)                                                         \
+  if ((rc = dispatch_one<n1, n2, f1, f3>(net, X, T, w, h, batch, params, grads, sq_err, A1, A2,  \
+                                         D2, slab, slab_bytes, s, query_only, need)) != 0)       \
+    return rc;
+  SRCNN_FUSED_CASE(64, 32, 9, 5)  // reference default (BASELINE.json configs[1])
+  SRCNN_FUSED_CASE(32, 16, 9, 5)  // example_config.json
+#undef SRCNN_FUSED_CASE
+  (void)lds_attr_set;
+  return 0;
+}
+
+}  // namespace fused
+}  // namespace srcnn

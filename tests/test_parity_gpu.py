@@ -304,11 +304,13 @@ def test_conv_grad_vs_oracle(S, path, shape):
 # ----------------------------------------------------------------------------
 # network level (ConfigBasedDataPipeline) vs the oracle
 # ----------------------------------------------------------------------------
-NETS = {"default": (64, 32, 9, 1, 5), "wide": (128, 64, 9, 5, 5), "tiny": (8, 4, 5, 1, 3)}
+NETS = {"default": (64, 32, 9, 1, 5), "wide": (128, 64, 9, 5, 5), "tiny": (8, 4, 5, 1, 3),
+        "example": (32, 16, 9, 1, 5)}
 
 
 @pytest.mark.parametrize("name,batch,size", [("default", 16, 33), ("wide", 3, 33), ("tiny", 5, 15),
-                                             ("default", 2, 48)])
+                                             ("default", 2, 48), ("example", 7, 33),
+                                             ("default", 3, 21), ("default", 600, 33)])
 def test_train_step_vs_oracle(S, path, name, batch, size):
     cfg = NETS[name]
     net = S.Net(*cfg)
