@@ -87,12 +87,37 @@ KERNEL_STAGES = {
 }
 
 
-def roofline_of(name, launches_per_step, ms_per_step, work, tiles, pmc=None):
+def fused_bytes(net, w, h):
+    """Minimum HBM bytes per tile of each fused kernel: every input it needs
+    read once, every output it produces written once (train_fused.hip)."""
+    n1, n2, f1, f2, f3 = net
+    w1, h1 = w - f1 + 1, h - f1 + 1
+    w3, h3 = w1 - f3 + 1, h1 - f3 + 1
+    X, A1, A2, T3 = 4 * w * h, 4 * w1 * h1 * n1, 4 * w1 * h1 * n2, 4 * w3 * h3
+    return {
+        "l12_fwd_mfma": X + A1 + A2,             # read X, write A1 and A2
+        "l3_delta_fused": A2 + T3 + A2,          # read A2 + centre of T, write delta2
+        "delta1_grad12_fused": X + A1 + A2,      # read X, A1, delta2 (delta1 never leaves the CU)
+    }
+
+
+def kernel_work(name, work, net, w, h):
+    """(algorithmic FLOPs, algorithmic HBM bytes) per tile of one kernel."""
     stages = KERNEL_STAGES.get(name)
-    if not stages or ms_per_step <= 0:
+    if not stages:
         return None
-    flops = sum(work[s][0] for s in stages) * tiles / launches_per_step
-    nbytes = sum(work[s][1] for s in stages) * tiles / launches_per_step
+    flops = sum(work[s][0] for s in stages)
+    nbytes = fused_bytes(net, w, h).get(name, sum(work[s][1] for s in stages))
+    return flops, nbytes
+
+
+def roofline_of(name, launches_per_step, ms_per_step, work, tiles, pmc=None, net=DEFAULT_NET,
+                w=TILE, h=TILE):
+    kw = kernel_work(name, work, net, w, h)
+    if not kw or ms_per_step <= 0:
+        return None
+    flops = kw[0] * tiles / launches_per_step
+    nbytes = kw[1] * tiles / launches_per_step
     dur_s = ms_per_step / launches_per_step * 1e-3
     traffic = None
     if pmc and name in pmc:

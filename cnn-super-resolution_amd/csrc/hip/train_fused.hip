@@ -175,200 +175,7 @@ __global__ __launch_bounds__(256, 2) void l12_fwd_kernel(
   }
 }
 
-// ---------------------------------------------------------------------------
-// Kernel 2: L3 forward + last-layer delta + delta2 + gW3/gB3 (+ squared error)
-// one sample per iteration, 8 waves, A2 tile resident in LDS
-// ---------------------------------------------------------------------------
-struct L3Geom {
-  int W, H;     // ground-truth sample (= network input size)
-  int w2, h2;   // A2
-  int w3, h3;   // A3
-  int batch;
-};
-
-template <int N2, int F3>
-__global__ __launch_bounds__(512, 1) void l3_delta_kernel(
-    const float* __restrict__ A2, const float* __restrict__ T, const float* __restrict__ W3,
-    const float* __restrict__ B3, float* __restrict__ D2, float* __restrict__ slab3,
-    float* __restrict__ sq_slab, L3Geom g) {
-  constexpr int K3 = F3 * F3, KS3 = (K3 + 1) / 2, NT2 = (N2 + 31) / 32;
-  constexpr int N2S = N2 + 4;      // padded A2 row: conflict-free ds_read_b128
-  constexpr int NW3 = K3 * N2;     // gW3 size; slab row = NW3 + 1 (gB3)
-  static_assert(K3 <= 32, "taps must fit one 32-row MFMA tile");
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int npx2 = g.w2 * g.h2, npx3 = g.w3 * g.h3;
-  const int w3p = g.w3 + 2 * (F3 - 1), h3p = g.h3 + 2 * (F3 - 1);
-  float* a2s = smem;                                   // [npx2][N2S]
-  float* d3p = smem + ((npx2 * N2S + 3) & ~3);         // [h3p][w3p], zero border
-  float* red = d3p + ((w3p * h3p + 3) & ~3);           // [1024] reduction scratch
-
-  const int lane = mfma::lane_id(), wave = mfma::wave_id();
-  const int h = lane >> 5, li = lane & 31;
-  const int nwaves = blockDim.x >> 6;
-  const int pad = (g.W - g.w3) / 2;  // last_layer_delta.cl:25
-
-  for (int i = threadIdx.x; i < w3p * h3p; i += blockDim.x) d3p[i] = 0.0f;
-
-  // delta2 B operands: W3[tap = 2s + h][n = 32u + li]
-  float w3f[KS3][NT2];
-#pragma unroll
-  for (int s = 0; s < KS3; s++)
-#pragma unroll
-    for (int u = 0; u < NT2; u++) {
-      const int tap = 2 * s + h, n = 32 * u + li;
-      w3f[s][u] = (tap < K3 && n < N2) ? W3[tap * N2 + n] : 0.0f;
-    }
-  // gW3 A-operand row of this lane: tap li
-  const int my_dy = li / F3, my_dx = li - (li / F3) * F3;
-  const bool my_tap = li < K3;
-
-  f32x16 gacc[NT2];
-#pragma unroll
-  for (int u = 0; u < NT2; u++) gacc[u] = zero16();
-  float gb3 = 0.0f, sq = 0.0f;
-  const float b3 = B3[0];
-
-  for (int sample = blockIdx.x; sample < g.batch; sample += gridDim.x) {
-    __syncthreads();
-    // A2 sample -> LDS (coalesced float4)
-    const float4* src = reinterpret_cast<const float4*>(A2 + (size_t)sample * npx2 * N2);
-    for (int i = threadIdx.x; i < npx2 * (N2 / 4); i += blockDim.x) {
-      const int p = i / (N2 / 4), q = i - p * (N2 / 4);
-      *reinterpret_cast<float4*>(a2s + p * N2S + 4 * q) = src[i];
-    }
-    __syncthreads();
-
-    // L3 forward (layer_uber_kernel.cl:70-91, SKIP_RELU) + last delta
-    // (last_layer_delta.cl:34-48) + squared error (squared_error.cl:60-69)
-    for (int o = threadIdx.x; o < npx3; o += blockDim.x) {
-      const int y = o / g.w3, x = o - y * g.w3;
-      float acc0 = 0.f, acc1 = 0.f;
-#pragma unroll
-      for (int dy = 0; dy < F3; dy++)
-#pragma unroll
-        for (int dx = 0; dx < F3; dx++) {
-          const float* ap = a2s + ((y + dy) * g.w2 + x + dx) * N2S;
-          const float* wp = W3 + (dy * F3 + dx) * N2;
-#pragma unroll
-          for (int q = 0; q < N2 / 4; q++) {
-            const float4 a = *reinterpret_cast<const float4*>(ap + 4 * q);
-            acc0 += a.x * wp[4 * q + 0];
-            acc1 += a.y * wp[4 * q + 1];
-            acc0 += a.z * wp[4 * q + 2];
-            acc1 += a.w * wp[4 * q + 3];
-          }
-        }
-      const float a3 = (acc0 + acc1) + b3;
-      const float t = T[(size_t)sample * g.W * g.H + (size_t)(y + pad) * g.W + x + pad];
-      const float diff = a3 - t;
-      const float d3 = diff * (a3 > 0.0f ? 1.0f : 0.0f);
-      d3p[(y + F3 - 1) * w3p + x + F3 - 1] = d3;
-      gb3 += d3;
-      sq += diff * diff;
-    }
-    __syncthreads();
-
-    // delta2 (layer_deltas.cl:79-123): per 32-pixel chunk of the A2 grid,
-    // D[pixel][n] = sum_tap d3p[pixel - tap] * W3[tap][n], masked by A2 > 0
-    const int nch = (npx2 + 31) / 32;
-    for (int c = wave; c < nch; c += nwaves) {
-      const int p = min(c * 32 + li, npx2 - 1);
-      const int y = p / g.w2, x = p - y * g.w2;
-      const int base = (y + F3 - 1) * w3p + x + F3 - 1;
-      f32x16 acc[NT2];
-#pragma unroll
-      for (int u = 0; u < NT2; u++) acc[u] = zero16();
-#pragma unroll
-      for (int s = 0; s < KS3; s++) {
-        const int k0 = 2 * s, k1 = 2 * s + 1;
-        const int o0 = (k0 / F3) * w3p + (k0 % F3);
-        const int o1 = k1 < K3 ? (k1 / F3) * w3p + (k1 % F3) : 0;
-        const float a = d3p[base - (h ? o1 : o0)];
-#pragma unroll
-        for (int u = 0; u < NT2; u++) acc[u] = mma(a, w3f[s][u], acc[u]);
-      }
-#pragma unroll
-      for (int r = 0; r < 16; r++) {
-        const int pr = c * 32 + crow(r, h);
-        if (pr < npx2) {
-#pragma unroll
-          for (int u = 0; u < NT2; u++) {
-            const int n = 32 * u + li;
-            if (n < N2) {
-              const float m = a2s[pr * N2S + n] > 0.0f ? 1.0f : 0.0f;
-              D2[((size_t)sample * npx2 + pr) * N2 + n] = acc[u][r] * m;
-            }
-          }
-        }
-      }
-    }
-
-    // gW3 (backpropagate.cl:89-106): G[tap][n] += sum_p' d3p[p' - tap] * A2[p'][n]
-    {
-      const int nks = (npx2 + 1) / 2;
-      int pp = 2 * wave + h;  // p' of this lane for k-step `wave`
-      int yq = pp / g.w2, xq = pp - yq * g.w2;
-      const int stride = 2 * nwaves;
-      for (int j = wave; j < nks; j += nwaves) {
-        const bool v = pp < npx2;
-        const float a = (v && my_tap) ? d3p[(yq - my_dy + F3 - 1) * w3p + xq - my_dx + F3 - 1] : 0.0f;
-#pragma unroll
-        for (int u = 0; u < NT2; u++) {
-          const int n = 32 * u + li;
-          const float b = (v && n < N2) ? a2s[pp * N2S + n] : 0.0f;
-          gacc[u] = mma(a, b, gacc[u]);
-        }
-        pp += stride;
-        xq += stride;
-        while (xq >= g.w2) {
-          xq -= g.w2;
-          yq++;
-        }
-      }
-    }
-  }
-
-  // ---- block reduction of the partial gradients, in wave order ----
-  __syncthreads();
-  for (int w = 0; w < nwaves; w++) {
-    if (wave == w) {
-#pragma unroll
-      for (int u = 0; u < NT2; u++)
-#pragma unroll
-        for (int r = 0; r < 16; r++) {
-          float* dst = red + (u * 16 + r) * 64 + lane;
-          *dst = (w == 0 ? 0.0f : *dst) + gacc[u][r];
-        }
-    }
-    __syncthreads();
-  }
-  float* out = slab3 + (size_t)blockIdx.x * (NW3 + 1);
-  for (int i = threadIdx.x; i < NT2 * 16 * 64; i += blockDim.x) {
-    const int u = i / 1024, r = (i >> 6) & 15, l = i & 63;
-    const int tap = crow(r, l >> 5), n = 32 * u + (l & 31);
-    if (tap < K3 && n < N2) out[tap * N2 + n] = red[i];
-  }
-  // gB3 and squared error: per-wave shuffle trees, then waves in order
-  for (int off = 32; off > 0; off >>= 1) {
-    gb3 += __shfl_down(gb3, off, 64);
-    sq += __shfl_down(sq, off, 64);
-  }
-  __syncthreads();
-  if (lane == 0) {
-    red[2 * wave] = gb3;
-    red[2 * wave + 1] = sq;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    float tb = 0.f, ts = 0.f;
-    for (int w = 0; w < nwaves; w++) {
-      tb += red[2 * w];
-      ts += red[2 * w + 1];
-    }
-    out[NW3] = tb;
-    sq_slab[blockIdx.x] = ts;
-  }
-}
+#include "l3_delta.hpp"
 
 // ---------------------------------------------------------------------------
 // Kernel 3: delta1 + gW2/gB2 + gW1/gB1
@@ -570,53 +377,62 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
     }
   }
 }
-
 // ---------------------------------------------------------------------------
-// deterministic slab reduction: grads[i] += sum_b slab[b][i] (block order)
+// deterministic slab reduction: dst[i] += sum_b slab[b][i]
+// block = 64 columns x 16 rows; row r sums slabs r, r+16, ... in order, then
+// the 16 row partials are added in row order (a fixed tree: bit-reproducible)
 // ---------------------------------------------------------------------------
-__global__ void slab_reduce_kernel(const float* __restrict__ slab12, int n12, int P12,
-                                   const float* __restrict__ slab3, int n3, int P3,
-                                   float* __restrict__ grads, const float* __restrict__ sq_slab,
-                                   float* __restrict__ sq_err) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < P12) {
-    float acc = 0.0f;
-    for (int b = 0; b < n12; b++) acc += slab12[(size_t)b * P12 + i];
-    grads[i] += acc;
-  } else if (i < P12 + P3) {
-    const int j = i - P12;
-    float acc = 0.0f;
-    for (int b = 0; b < n3; b++) acc += slab3[(size_t)b * P3 + j];
-    grads[i] += acc;
-  } else if (i == P12 + P3 && sq_err) {
-    float acc = 0.0f;
-    for (int b = 0; b < n3; b++) acc += sq_slab[b];
-    *sq_err += acc;
+__global__ __launch_bounds__(1024) void slab_reduce_kernel(const float* __restrict__ slab, int nslab,
+                                                           int P, float* __restrict__ dst) {
+  __shared__ float part[16][65];
+  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int row = threadIdx.x >> 6;
+  float acc = 0.0f;
+  if (col < P)
+    for (int b = row; b < nslab; b += 16) acc += slab[(size_t)b * P + col];
+  part[row][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (row == 0 && col < P) {
+    float t = 0.0f;
+#pragma unroll
+    for (int r = 0; r < 16; r++) t += part[r][threadIdx.x];
+    dst[col] += t;
   }
+}
+
+static int reduce_slabs(const float* slab, int nslab, int P, float* dst, hipStream_t s) {
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3((P + 63) / 64), dim3(1024), 0, s, slab, nslab, P, dst);
+  SRCNN_LAUNCH_TRY();
+  return SRCNN_OK;
 }
 
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
-struct Plan {
-  int grid12, grid3, grid_d1;
-  size_t l3_lds;
-  size_t slab12_floats, slab3_floats;
-};
-
 template <int N1, int N2, int F1, int F3>
 struct Net {
   static constexpr int P12 = F1 * F1 * N1 + N1 + N1 * N2 + N2;
   static constexpr int P3 = F3 * F3 * N2 + 1;
 };
 
-static size_t l3_lds_bytes(int npx2, int n2, int w3p, int h3p) {
-  const size_t a2 = ((size_t)npx2 * (n2 + 4) + 3) & ~size_t(3);
-  const size_t d3 = ((size_t)w3p * h3p + 3) & ~size_t(3);
-  return (a2 + d3 + 1024) * sizeof(float);
-}
-
 static int grid_for_batch(uint32_t batch, int cap) { return (int)std::min<uint32_t>(batch, cap); }
+
+template <int N2, int F3, int PF>
+static int launch_l3(const float* A2, const float* T, const float* W3, const float* B3, float* D2,
+                     float* slab3, float* sqs, const L3Geom& lg, int grid, size_t lds, hipStream_t s) {
+  static bool attr = false;  // the A2 tile exceeds the 64 KiB default dynamic LDS
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)l3_delta_kernel<N2, F3, PF>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess)
+      return fail(SRCNN_ERR_HIP, "hipFuncSetAttribute(l3_delta): %s", hipGetErrorString(e));
+    attr = true;
+  }
+  hipLaunchKernelGGL((l3_delta_kernel<N2, F3, PF>), dim3(grid), dim3(kL3Threads), lds, s, A2, T,
+                     W3, B3, D2, slab3, sqs, lg);
+  SRCNN_LAUNCH_TRY();
+  return SRCNN_OK;
+}
 
 // Returns 1 if the shape is specialised (and the step was enqueued), 0 if
 // not (caller falls back to the op-by-op path), <0 on error.
@@ -628,7 +444,10 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   const int ow = w - F1 + 1, oh = h - F1 + 1;
   const int w3 = ow - F3 + 1, h3 = oh - F3 + 1;
   if ((int)(w * h) > kXsMax || w3 <= 0 || h3 <= 0) return 0;
-  const size_t lds3 = l3_lds_bytes(ow * oh, N2, w3 + 2 * (F3 - 1), h3 + 2 * (F3 - 1));
+  const int npx2 = ow * oh;
+  const int pf = l3_prefetch_regs<N2, F3>(npx2);
+  if (pf > 16) return 0;
+  const size_t lds3 = l3_lds_bytes<N2, F3>(npx2, w3, h3);
   if (lds3 > 160 * 1024) return 0;
   const int g12 = grid_for_batch(batch, 1024);
   const int g3 = grid_for_batch(batch, 256);
@@ -661,9 +480,9 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   L3Geom lg{(int)w, (int)h, ow, oh, w3, h3, (int)batch};
   {
     SRCNN_PROFILE("l3_delta_fused", s);
-    hipLaunchKernelGGL((l3_delta_kernel<N2, F3>), dim3(g3), dim3(512), lds3, s, A2, T, W3, B3, D2,
-                       slab3, sqs, lg);
-    SRCNN_LAUNCH_TRY();
+    int rc = pf <= 10 ? launch_l3<N2, F3, 10>(A2, T, W3, B3, D2, slab3, sqs, lg, g3, lds3, s)
+                      : launch_l3<N2, F3, 16>(A2, T, W3, B3, D2, slab3, sqs, lg, g3, lds3, s);
+    if (rc) return rc;
   }
   {
     SRCNN_PROFILE("delta1_grad12_fused", s);
@@ -673,15 +492,13 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   }
   {
     SRCNN_PROFILE("slab_reduce", s);
-    const int tot = NetT::P12 + NetT::P3 + 1;
-    hipLaunchKernelGGL(slab_reduce_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, slab12, gd,
-                       NetT::P12, slab3, g3, NetT::P3, grads, sqs, sq_err);
-    SRCNN_LAUNCH_TRY();
+    int rc = reduce_slabs(slab12, gd, NetT::P12, grads, s);
+    if (!rc) rc = reduce_slabs(slab3, g3, NetT::P3, grads + NetT::P12, s);
+    if (!rc && sq_err) rc = reduce_slabs(sqs, g3, 1, sq_err, s);
+    if (rc) return rc;
   }
   return 1;
 }
-
-static bool lds_attr_set = false;
 
 template <int N1, int N2, int F1, int F3>
 static int dispatch_one(const srcnn_net* net, const float* X, const float* T, uint32_t w,
@@ -691,13 +508,6 @@ static int dispatch_one(const srcnn_net* net, const float* X, const float* T, ui
   if (net->n1 != (uint32_t)N1 || net->n2 != (uint32_t)N2 || net->f1 != (uint32_t)F1 ||
       net->f2 != 1 || net->f3 != (uint32_t)F3)
     return 0;
-  if (!query_only) {
-    // the L3 kernel keeps a whole A2 sample in LDS (> 64 KiB default)
-    hipError_t e = hipFuncSetAttribute((const void*)l3_delta_kernel<N2, F3>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (e != hipSuccess)
-      return fail(SRCNN_ERR_HIP, "hipFuncSetAttribute(l3_delta): %s", hipGetErrorString(e));
-  }
   return run<N1, N2, F1, F3>(X, T, w, h, batch, params, grads, sq_err, A1, A2, D2, slab,
                              slab_bytes, s, query_only, need);
 }
@@ -714,7 +524,6 @@ int train_fwd_bwd(const srcnn_net* net, const float* X, const float* T, uint32_t
   SRCNN_FUSED_CASE(64, 32, 9, 5)  // reference default (BASELINE.json configs[1])
   SRCNN_FUSED_CASE(32, 16, 9, 5)  // example_config.json
 #undef SRCNN_FUSED_CASE
-  (void)lds_attr_set;
   return 0;
 }
 
