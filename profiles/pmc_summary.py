@@ -1,0 +1,88 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 PMC passes (tools/pmc_session.sh) per kernel.
+
+    python profiles/pmc_summary.py gpurun_out/<tag>/pmc profiles/pmc_<round>.json
+
+HBM bytes per launch follow MI355X_MICROARCH.md "HBM": FETCH_SIZE and
+WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reads exactly half the bytes of
+wide coalesced streaming reads, so the read side is doubled.  WRITE_SIZE is
+exact for 16-B/lane streaming stores; our narrower stores are uncalibrated,
+so the figure is an estimate (ratios between variants are exact).
+"""
+import csv
+import glob
+import json
+import os
+import re
+import sys
+from collections import defaultdict
+
+SHORT = [
+    (r"l12_fwd_kernel", "l12_fwd_mfma"),
+    (r"l3_delta_kernel", "l3_delta_fused"),
+    (r"d1_grad12_kernel", "delta1_grad12_fused"),
+    (r"slab_reduce_kernel", "slab_reduce"),
+    (r"sgd_update_kernel", "sgd_update"),
+    (r"update_all_kernel", "update_all"),
+    (r"fill_kernel", "fill"),
+    (r"generic::conv_fwd_kernel", "conv_fwd_generic"),
+    (r"generic::conv_delta_kernel", "conv_delta_generic"),
+    (r"generic::grad_partial_kernel", "grad_partial_generic"),
+    (r"generic::grad_reduce_kernel", "grad_reduce_generic"),
+]
+
+
+def short(name):
+    for pat, s in SHORT:
+        if re.search(pat, name):
+            return s
+    return None
+
+
+def main(src, dst):
+    vals = defaultdict(lambda: defaultdict(list))  # kernel -> counter -> per-dispatch values
+    durs = defaultdict(dict)
+    for f in glob.glob(os.path.join(src, "*", "run_counter_collection.csv")):
+        per = defaultdict(lambda: defaultdict(float))
+        for row in csv.DictReader(open(f)):
+            k = short(row["Kernel_Name"])
+            if not k:
+                continue
+            key = (k, row["Dispatch_Id"])
+            per[key][row["Counter_Name"]] += float(row["Counter_Value"])
+            durs[k][row["Dispatch_Id"] + os.path.dirname(f)] = (
+                int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
+        for (k, _), cs in per.items():
+            for c, v in cs.items():
+                vals[k][c].append(v)
+    out = {"source": "rocprofv3 --pmc (tools/pmc_session.sh), per-dispatch means",
+           "hbm_note": "hbm_bytes_per_launch = (2*FETCH_SIZE + WRITE_SIZE) * 1024 "
+                       "(gfx950 FETCH_SIZE halving, MI355X_MICROARCH.md HBM)",
+           "kernels": {}}
+    for k, cs in sorted(vals.items()):
+        m = {c: sum(v) / len(v) for c, v in cs.items()}
+        d = list(durs[k].values())
+        rec = {"dispatches": max(len(v) for v in cs.values()), "counters": m,
+               "mean_duration_us": (sum(d) / len(d) / 1e3) if d else None}
+        if "FETCH_SIZE" in m and "WRITE_SIZE" in m:
+            rec["hbm_bytes_per_launch"] = int((2 * m["FETCH_SIZE"] + m["WRITE_SIZE"]) * 1024)
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in m and "GRBM_GUI_ACTIVE" in m and m["GRBM_GUI_ACTIVE"]:
+            # MFMA busy cycles summed over SIMDs / (SIMDs * active cycles)
+            rec["mfma_busy_frac"] = m["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024.0 * m["GRBM_GUI_ACTIVE"] / 8)
+        if "SQ_LDS_BANK_CONFLICT" in m and m.get("SQ_LDS_IDX_ACTIVE"):
+            rec["lds_conflict_frac"] = m["SQ_LDS_BANK_CONFLICT"] / m["SQ_LDS_IDX_ACTIVE"]
+        if "SQ_WAVE_CYCLES" in m and m["SQ_WAVE_CYCLES"]:
+            rec["wait_any_frac"] = m.get("SQ_WAIT_ANY", 0) / m["SQ_WAVE_CYCLES"]
+            rec["wait_inst_frac"] = m.get("SQ_WAIT_INST_ANY", 0) / m["SQ_WAVE_CYCLES"]
+            rec["active_frac"] = m.get("SQ_ACTIVE_INST_ANY", 0) / m["SQ_WAVE_CYCLES"]
+        if "GRBM_GUI_ACTIVE" in m and d:
+            rec["eff_clock_ghz"] = m["GRBM_GUI_ACTIVE"] / 8 / (sum(d) / len(d))
+        out["kernels"][k] = rec
+    with open(dst, "w") as fh:
+        json.dump(out, fh, indent=1)
+    for k, r in out["kernels"].items():
+        print(k, {x: (round(y, 4) if isinstance(y, float) else y) for x, y in r.items() if x != "counters"})
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
