@@ -16,6 +16,7 @@ struct L3Geom {
   int w2, h2;   // A2
   int w3, h3;   // A3
   int batch;
+  int ablate;   // diagnostics only (env SRCNN_ABLATE_L3): bit0 L3, bit1 delta2, bit2 gW3
 };
 
 constexpr int kL3Threads = 512;
@@ -97,7 +98,7 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
     __syncthreads();
 
     // ---- L3 forward + last delta + squared error ----
-    for (int it = item0; it < nitems; it += items_per_pass) {
+    for (int it = item0; (g.ablate & 1) == 0 && it < nitems; it += items_per_pass) {
       const int y = it / nseg, x0 = (it - y * nseg) * kL3Seg;
       float acc[kL3Seg];
 #pragma unroll
@@ -143,7 +144,7 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
 
     // ---- delta2: per 32-pixel chunk of the A2 grid ----
     const int nch = (npx2 + 31) / 32;
-    for (int c = wave; c < nch; c += nwaves) {
+    for (int c = wave; (g.ablate & 2) == 0 && c < nch; c += nwaves) {
       const int p = min(c * 32 + li, npx2 - 1);
       const int y = p / g.w2, x = p - y * g.w2;
       const int base = (y + F3 - 1) * w3p + x + F3 - 1;
@@ -183,7 +184,7 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
 
     // ---- gW3: G[tap][n] += sum_p' d3p[p' - tap] * A2[p'][n] ----
     {
-      const int nks = (npx2 + 1) / 2;
+      const int nks = (g.ablate & 4) ? 0 : (npx2 + 1) / 2;
       int pp = 2 * wave + h;
       int yq = pp / g.w2, xq = pp - yq * g.w2;
       const int stride = 2 * nwaves;

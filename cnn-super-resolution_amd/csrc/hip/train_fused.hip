@@ -23,6 +23,8 @@
 // layer-by-layer dataflow.  Results are deterministic: the
 // sample -> block -> wave assignment is static and every sum has a fixed
 // order; no float atomics anywhere.
+#include <cstdlib>
+
 #include "common.hpp"
 #include "mfma.hpp"
 #include "ops.hpp"
@@ -35,7 +37,7 @@ using mfma::f32x16;
 using mfma::mma;
 using mfma::zero16;
 
-constexpr int kXsMax = 2048;  // input sample / region tile (floats) staged in LDS
+constexpr int kXsMax = 1536;  // input sample / region tile (floats) staged in LDS (<= 39x39)
 
 struct Geom {
   int W, H;      // input sample
@@ -175,6 +177,7 @@ __global__ __launch_bounds__(256, 2) void l12_fwd_kernel(
   }
 }
 
+
 #include "l3_delta.hpp"
 
 // ---------------------------------------------------------------------------
@@ -193,12 +196,14 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
   constexpr int P12 = NW1 + N1 + NW2 + N2;  // [gW1 | gB1 | gW2 | gB2]
   constexpr int RED = (MT * NT1 + NT1 * NT2) * 16 * 64;
   static_assert(N2 % 2 == 0, "n2 must be even");
-  constexpr int LDS_MAIN = kXsMax + N1 * WS + 4 * 32 * DS;
+  constexpr int A1S = 4 * 32 * N1;        // per-wave A1 chunk staging (LDS-DMA target)
+  constexpr int LDS_MAIN = A1S + kXsMax + N1 * WS + 4 * 32 * DS;
   constexpr int LDS_TOTAL = LDS_MAIN > RED ? LDS_MAIN : RED;
   __shared__ __attribute__((aligned(16))) float smem[LDS_TOTAL];
   __shared__ int xbt[4][32];
-  float* xs = smem;
-  float* w2s = smem + kXsMax;          // [N1][WS]: W2[c][n]
+  float* a1s = smem;                   // [4][32][N1], lane-linear DMA image of A1 rows
+  float* xs = smem + A1S;
+  float* w2s = xs + kXsMax;            // [N1][WS]: W2[c][n]
   float* d2w = w2s + N1 * WS;          // [4][32][DS]
 
   const int lane = mfma::lane_id(), wave = mfma::wave_id();
@@ -211,12 +216,13 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
   }
   // gW1 A-operand rows of this lane: taps 32m + li (tap K1 = ones -> gB1)
   int toff[MT];
-  float tsel[MT];  // 0: zero row, 1: X tap, 2: ones row
+  float tsel_x[MT], tsel_1[MT];  // a = X * tsel_x + tsel_1: X tap / zero row / ones row
 #pragma unroll
   for (int m = 0; m < MT; m++) {
     const int tap = 32 * m + li;
     toff[m] = tap < K1 ? (tap / F1) * g.W + (tap % F1) : 0;
-    tsel[m] = tap < K1 ? 1.0f : (tap == K1 ? 2.0f : 0.0f);
+    tsel_x[m] = tap < K1 ? 1.0f : 0.0f;
+    tsel_1[m] = tap == K1 ? 1.0f : 0.0f;
   }
 
   f32x16 g1[MT][NT1], g2[NT1][NT2];
@@ -233,13 +239,36 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
   for (int u = 0; u < NT2; u++) gb2[u] = 0.0f;
 
   float* d2me = d2w + wave * 32 * DS;
+  // A1 rows of one chunk -> this wave's LDS image by LDS-DMA (no registers):
+  // instruction k moves floats [256k, 256k + 256) of the [32][N1] chunk; rows
+  // past the sample re-read its last row (finite, and their delta2 rows are 0)
+  float* a1me = a1s + wave * 32 * N1;
+#define SRCNN_D1_A1_DMA(SMP, C)                                                   \
+  do {                                                                            \
+    int lo_ = 4 * lane; /* opaque: keeps the addresses out of the loop preheader */ \
+    asm volatile("" : "+v"(lo_));                                                 \
+    const float* base_ = A1 + (size_t)(SMP) * npx * N1;                           \
+    _Pragma("unroll") for (int k = 0; k < 32 * N1 / 256; k++) {                   \
+      const int f_ = k * 256 + lo_;                                               \
+      const int row_ = min((C) * 32 + f_ / N1, npx - 1);                          \
+      const float* src_ = base_ + (row_ * N1 + (f_ % N1));                        \
+      __builtin_amdgcn_global_load_lds(                                           \
+          (const void*)src_, (__attribute__((address_space(3))) void*)(a1me + k * 256), 16, 0, 0); \
+    }                                                                             \
+  } while (0)
+  const int nch = (npx + 31) / 32;
+  // A1[p][c] of this lane's accumulator slots, read from the LDS image at use
+#define SRCNN_D1_A1(T, R) a1me[crow(R, h) * N1 + 32 * (T) + li]
+
   for (int sample = blockIdx.x; sample < g.batch; sample += gridDim.x) {
     __syncthreads();
-    const float* xsrc = X + (size_t)sample * g.W * g.H;
-    for (int i = threadIdx.x; i < g.W * g.H; i += blockDim.x) xs[i] = xsrc[i];
+    if (wave < nch) SRCNN_D1_A1_DMA(sample, wave);
+    {
+      const float* src = X + (size_t)sample * g.W * g.H;
+      for (int i = threadIdx.x; i < g.W * g.H; i += 256) xs[i] = src[i];
+    }
     __syncthreads();
 
-    const int nch = (npx + 31) / 32;
     for (int c = wave; c < nch; c += 4) {
       {  // this lane's own pixel -> X base offset table
         const int p = min(c * 32 + li, npx - 1);
@@ -258,15 +287,9 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
         d[2] = v.z;
         d[3] = v.w;
       }
-      // A1 in accumulator layout: a1[t][r] = A1[pixel crow(r,h)][32t + li]
-      float a1[NT1][16];
-#pragma unroll
-      for (int r = 0; r < 16; r++) {
-        const int pr = c * 32 + crow(r, h);
-#pragma unroll
-        for (int t = 0; t < NT1; t++)
-          a1[t][r] = pr < npx ? A1[((size_t)sample * npx + pr) * N1 + 32 * t + li] : 0.0f;
-      }
+      // the A1 DMA of this chunk has landed (the delta2 loads above already
+      // waited for the older VM ops; keep the wait explicit for the DMA)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_wave_barrier();
 
       // delta1[p][c] = [A1 > 0] * sum_n delta2[p][n] * W2[c][n]  (layer_deltas.cl, f=1)
@@ -286,7 +309,7 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
 #pragma unroll
       for (int t = 0; t < NT1; t++)
 #pragma unroll
-        for (int r = 0; r < 16; r++) d1[t][r] = a1[t][r] > 0.0f ? d1[t][r] : 0.0f;
+        for (int r = 0; r < 16; r++) d1[t][r] = SRCNN_D1_A1(t, r) > 0.0f ? d1[t][r] : 0.0f;
 
       // gW2[c][n] += sum_p A1[p][c] delta2[p][n]; gB2[n] += sum_p delta2[p][n]
 #pragma unroll
@@ -298,24 +321,35 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
           const float b = n < N2 ? d2me[pr * DS + n] : 0.0f;
           gb2[u] += b;
 #pragma unroll
-          for (int t = 0; t < NT1; t++) g2[t][u] = mma(a1[t][s], b, g2[t][u]);
+          for (int t = 0; t < NT1; t++) g2[t][u] = mma(SRCNN_D1_A1(t, s), b, g2[t][u]);
         }
       }
+
+      // next chunk's A1 DMA overlaps the gW1 MFMAs (the image's reads retired)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      if (c + 4 < nch) SRCNN_D1_A1_DMA(sample, c + 4);
+
       // gW1[tap][c] += sum_p X[p + tap] delta1[p][c]; ones row -> gB1[c]
 #pragma unroll
       for (int s = 0; s < 16; s++) {
         const int xb = xbt[wave][crow(s, h)];
 #pragma unroll
         for (int m = 0; m < MT; m++) {
-          const float xv = xs[xb + toff[m]];
-          const float a = tsel[m] == 1.0f ? xv : (tsel[m] == 2.0f ? 1.0f : 0.0f);
+          float a = xs[xb + toff[m]];
+          if (32 * m + 31 >= K1) a = tsel_x[m] != 0.0f ? a : tsel_1[m];  // zero rows / ones row
 #pragma unroll
           for (int t = 0; t < NT1; t++) g1[m][t] = mma(a, d1[t][s], g1[m][t]);
         }
+#ifdef SRCNN_D1_SCHED
+        if ((s & (SRCNN_D1_SCHED - 1)) == SRCNN_D1_SCHED - 1) __builtin_amdgcn_sched_barrier(0);
+#endif
       }
       __builtin_amdgcn_wave_barrier();
     }
   }
+#undef SRCNN_D1_A1_DMA
+#undef SRCNN_D1_A1
 
   // ---- block reduction (waves in order) into LDS, then one slab per block ----
   __syncthreads();
@@ -477,7 +511,11 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
                        B1, W2, B2, A1, A2, g);
     SRCNN_LAUNCH_TRY();
   }
-  L3Geom lg{(int)w, (int)h, ow, oh, w3, h3, (int)batch};
+  static const int l3_ablate = [] {
+    const char* e = getenv("SRCNN_ABLATE_L3");  // diagnostics only
+    return e ? atoi(e) : 0;
+  }();
+  L3Geom lg{(int)w, (int)h, ow, oh, w3, h3, (int)batch, l3_ablate};
   {
     SRCNN_PROFILE("l3_delta_fused", s);
     int rc = pf <= 10 ? launch_l3<N2, F3, 10>(A2, T, W3, B3, D2, slab3, sqs, lg, g3, lds3, s)
