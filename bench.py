@@ -77,7 +77,7 @@ KERNEL_STAGES = {
     "l2_fwd_mfma": ["l2_fwd"],
     "l3_fwd": ["l3_fwd"],
     "l12_fwd_mfma": ["l1_fwd", "l2_fwd"],
-    "l3_delta_fused": ["l3_fwd", "last_delta", "delta2"],
+    "l3_delta_fused": ["l3_fwd", "last_delta", "delta2", "grad3"],
     "delta2": ["delta2"],
     "delta1_mfma": ["delta1"],
     "grad1_mfma": ["grad1"],
@@ -210,17 +210,12 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
-
     import srcnn_amd as S
+    from srcnn_amd import parallel
+
+    rank, world, local = parallel.env_world()
+    torch.cuda.set_device(local if world > 1 else 0)
+    parallel.init("nccl", torch.device("cuda", local))
     S.set_path(0 if args.path == "auto" else 1)
     dev = torch.device("cuda", torch.cuda.current_device())
     stream = torch.cuda.current_stream().cuda_stream
@@ -242,11 +237,13 @@ def main():
     lr = [1e-4, 1e-4, 1e-5]
     global_tiles = B * world
 
-    def step():
-        S.train_fwd_bwd(net, Xd, Td, w, h, B, params, grads, None, ws, ws_bytes, stream)
-        if world > 1:
-            dist.all_reduce(grads)
-        S.update_all(net, params, grads, mom, 0.9, 1e-3, lr, global_tiles, stream)
+    # one rank's shard of the global batch -> grads; one all-reduce; the same
+    # update on every rank (srcnn_amd/parallel.py)
+    step = parallel.DataParallelStep(
+        grads,
+        lambda g: S.train_fwd_bwd(net, Xd, Td, w, h, B, params, g, None, ws, ws_bytes, stream),
+        lambda nb: S.update_all(net, params, grads, mom, 0.9, 1e-3, lr, nb, stream),
+        global_tiles)
 
     for _ in range(args.warmup):
         step()

@@ -284,7 +284,7 @@ int srcnn_train_fwd_bwd(const srcnn_net* net, const float* X, const float* T, ui
                                      false, nullptr);
     if (rc != 0) return rc < 0 ? rc : SRCNN_OK;
   }
-  // forward: ConfigBasedDataPipeline.cpp:375-397
+  // forward: ConfigBasedDataPipeline.cpp:200-241
   if ((rc = srcnn_conv_fwd(X, A1, W1, B1, w, h, 1, net->n1, net->f1, 1, batch, stream))) return rc;
   if ((rc = srcnn_conv_fwd(A1, A2, W2, B2, d.w1, d.h1, net->n1, net->n2, net->f2, 1, batch, stream)))
     return rc;
@@ -294,7 +294,7 @@ int srcnn_train_fwd_bwd(const srcnn_net* net, const float* X, const float* T, ui
       (rc = srcnn::reduce(2, A3, T, d.s3 * batch, w, h, d.w3, d.h3, sq_err, 1, gws, gws_bytes,
                           srcnn::as_stream(stream))))
     return rc;
-  // backward: ConfigBasedDataPipeline.cpp:420-479
+  // backward: ConfigBasedDataPipeline.cpp:243-323
   if ((rc = srcnn_last_delta(T, A3, D3, w, h, d.w3, d.h3, batch, stream))) return rc;
   if ((rc = srcnn_conv_delta(D3, A2, D2, W3, net->f3, net->n2, 1, d.w2, d.h2, batch, stream)))
     return rc;
@@ -317,7 +317,7 @@ int srcnn_update_all(const srcnn_net* net, float* params, float* grads, float* m
   size_t off[6];
   srcnn_net_offsets(net, off);
   const size_t total = off[5] + 1;
-  // layer 3, 2, 1: ConfigBasedDataPipeline.cpp:491-508
+  // layer 3, 2, 1: ConfigBasedDataPipeline.cpp:325-361
   for (int l = 2; l >= 0; l--) {
     const size_t wo = off[2 * l], bo = off[2 * l + 1];
     const size_t end = l == 2 ? total : off[2 * l + 2];

@@ -34,7 +34,7 @@ _S = ctypes.c_size_t
 
 
 class Net(ctypes.Structure):
-    """srcnn_net: Config n1, n2, f1, f2, f3 (reference src/Config.hpp:402-403)."""
+    """srcnn_net: Config n1, n2, f1, f2, f3 (reference src/Config.hpp:27-28)."""
     _fields_ = [("n1", _U), ("n2", _U), ("f1", _U), ("f2", _U), ("f3", _U)]
 
     def __repr__(self):

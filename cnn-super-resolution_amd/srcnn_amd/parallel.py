@@ -1,0 +1,73 @@
+"""Data-parallel training step: one process per GPU, one gradient all-reduce.
+
+SURVEY.md 8(e): tiles are independent, so a step shards the tile batch over
+ranks (contiguous slices, rank r takes [r*B/N, (r+1)*B/N)), each rank
+accumulates the gradients of its slice into the flat buffer
+[gW1|gB1|gW2|gB2|gW3|gB3], ONE all-reduce(SUM) combines them (RCCL over xGMI
+with the "nccl" backend; gloo in the CPU tests), and every rank applies the
+same update with batch = global tile count, so the parameter replicas stay
+identical.  This replaces the reference's single-queue
+`execute_batch -> update_parameters` sequence
+(src/ConfigBasedDataPipeline.cpp:128-195, :325-361; src/Main_cl.cpp:157-195)
+for N devices.
+
+Compute is injected (`fwd_bwd(grads)`, `update(batch)`): on a GPU these are
+`srcnn_amd.train_fwd_bwd` / `srcnn_amd.update_all` on the HIP stream the
+collective runs on; nothing here computes anything itself.
+"""
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def env_world():
+    """(rank, world_size, local_rank) from the torch.distributed.run env."""
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def init(backend, device=None):
+    """init_process_group from the env (MASTER_ADDR defaults to 127.0.0.1)."""
+    rank, world, _ = env_world()
+    if world <= 1:
+        return rank, world
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    kw = {"device_id": device} if device is not None and backend == "nccl" else {}
+    dist.init_process_group(backend, rank=rank, world_size=world, **kw)
+    return rank, world
+
+
+def shard(global_batch, rank, world):
+    """Contiguous slice [start, start+count) of the global tile batch for `rank`
+    (the remainder goes to the lowest ranks, one tile each)."""
+    if global_batch < 0 or world < 1 or not 0 <= rank < world:
+        raise ValueError("bad shard request")
+    base, rem = divmod(global_batch, world)
+    start = rank * base + min(rank, rem)
+    return start, base + (1 if rank < rem else 0)
+
+
+class DataParallelStep:
+    """fwd_bwd(grads) accumulates this rank's gradients; update(global_batch)
+    applies the SGD step and zeroes the gradients (srcnn_update_all)."""
+
+    def __init__(self, grads, fwd_bwd, update, global_batch, group=None):
+        if not isinstance(grads, torch.Tensor) or grads.dtype != torch.float32:
+            raise TypeError("grads must be a float32 tensor (the flat gradient buffer)")
+        self.grads = grads
+        self.fwd_bwd = fwd_bwd
+        self.update = update
+        self.global_batch = int(global_batch)
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+
+    def allreduce(self):
+        """Sum the flat gradient buffer over ranks (one collective per step)."""
+        if self.world > 1:
+            dist.all_reduce(self.grads, op=dist.ReduceOp.SUM, group=self.group)
+
+    def __call__(self):
+        self.fwd_bwd(self.grads)
+        self.allreduce()
+        self.update(self.global_batch)

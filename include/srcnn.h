@@ -162,7 +162,7 @@ SRCNN_API int srcnn_swap_luma(const uint8_t* rgba, const float* new_luma,
 
 /* ---- network level: ConfigBasedDataPipeline (src/ConfigBasedDataPipeline.cpp) ---- */
 typedef struct srcnn_net {
-  uint32_t n1, n2, f1, f2, f3; /* Config n1,n2,f1,f2,f3 (src/Config.hpp:402-403) */
+  uint32_t n1, n2, f1, f2, f3; /* Config n1,n2,f1,f2,f3 (src/Config.hpp:27-28) */
 } srcnn_net;
 
 /* offsets (in floats) of W1,B1,W2,B2,W3,B3 inside the flat parameter buffer */
@@ -170,8 +170,8 @@ SRCNN_API int srcnn_net_offsets(const srcnn_net* net, size_t offsets[6]);
 SRCNN_API size_t srcnn_net_param_count(const srcnn_net* net);
 
 /* One chunk of ConfigBasedDataPipeline::execute_batch(backpropagate=true)
- * (src/ConfigBasedDataPipeline.cpp:287-355): forward L1..L3 (:359-400),
- * last-layer delta, deltas and gradients (:402-482).  Gradients are
+ * (src/ConfigBasedDataPipeline.cpp:128-195): forward L1..L3 (:200-241),
+ * last-layer delta, deltas and gradients (:243-323).  Gradients are
  * ACCUMULATED into `grads` (flat layout).  X = mean-subtracted input luma,
  * T = ground-truth luma, both [batch][h][w].  If sq_err != NULL the chunk's
  * squared error (validation metric) is ADDED to *sq_err (device). */
@@ -183,15 +183,15 @@ SRCNN_API int srcnn_train_fwd_bwd(const srcnn_net* net, const float* X,
                                   float* grads, float* sq_err, void* ws,
                                   size_t ws_bytes, srcnn_stream_t stream);
 
-/* ConfigBasedDataPipeline::update_parameters (src/ConfigBasedDataPipeline.cpp:484-520):
+/* ConfigBasedDataPipeline::update_parameters (src/ConfigBasedDataPipeline.cpp:325-361):
  * update all layers with per-layer lr[3], shared momentum / wd, then zero
- * the gradient accumulators (:511-517). */
+ * the gradient accumulators (:353-358). */
 SRCNN_API int srcnn_update_all(const srcnn_net* net, float* params,
                                float* grads, float* momentum_bufs,
                                float momentum, float wd, const float* lr,
                                uint32_t batch, srcnn_stream_t stream);
 
-/* Forward / inference (src/ConfigBasedDataPipeline.cpp:273-285, :359-400):
+/* Forward / inference (src/ConfigBasedDataPipeline.cpp:114-126, :200-241):
  * out = A3 [batch][h-pad][w-pad], pad = f1+f2+f3-3. */
 SRCNN_API size_t srcnn_forward_workspace_bytes(const srcnn_net* net,
                                                uint32_t w, uint32_t h,

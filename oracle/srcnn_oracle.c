@@ -292,7 +292,7 @@ size_t oracle_param_count(int n1, int n2, int f1, int f2, int f3) {
          (size_t)f3 * f3 * n2 * 1 + 1;
 }
 
-/* LayerData(1,n1,f1), (n1,n2,f2), (n2,1,f3): ConfigBasedDataPipeline.cpp:187-189 */
+/* LayerData(1,n1,f1), (n1,n2,f2), (n2,1,f3): ConfigBasedDataPipeline.cpp:27-29 */
 static void layer_offsets(int n1, int n2, int f1, int f2, int f3,
                           size_t off[6]) {
   off[0] = 0;                                   /* W1 */
@@ -308,7 +308,7 @@ size_t oracle_train_acts_floats(int n1, int n2, int f1, int f2, int f3,
   const size_t o1 = (size_t)(w - f1 + 1) * (h - f1 + 1);
   const size_t o2 = (size_t)(w - f1 - f2 + 2) * (h - f1 - f2 + 2);
   const size_t o3 = (size_t)(w - f1 - f2 - f3 + 3) * (h - f1 - f2 - f3 + 3);
-  /* A1, A2, A3, D3, D2, D1 (ConfigBasedDataPipeline.cpp:249-265) */
+  /* A1, A2, A3, D3, D2, D1 (ConfigBasedDataPipeline.cpp:82-108) */
   return (size_t)batch * (2 * o1 * n1 + 2 * o2 * n2 + 2 * o3);
 }
 
@@ -329,11 +329,11 @@ void oracle_train_fwd_bwd(int n1, int n2, int f1, int f2, int f3,
                                      oracle_train_acts_floats(n1, n2, f1, f2, f3, w, h, batch));
   float *A1 = buf, *A2 = A1 + s1, *A3 = A2 + s2, *D3 = A3 + s3, *D2 = D3 + s3,
         *D1 = D2 + s2;
-  /* forward, ConfigBasedDataPipeline.cpp:375-397 */
+  /* forward, ConfigBasedDataPipeline.cpp:200-241 */
   oracle_conv_fwd(X, A1, params + off[0], params + off[1], w, h, 1, n1, f1, 1, batch);
   oracle_conv_fwd(A1, A2, params + off[2], params + off[3], w1, h1, n1, n2, f2, 1, batch);
   oracle_conv_fwd(A2, A3, params + off[4], params + off[5], w2, h2, n2, 1, f3, 0, batch);
-  /* backward, ConfigBasedDataPipeline.cpp:420-479 */
+  /* backward, ConfigBasedDataPipeline.cpp:243-323 */
   oracle_last_delta(T, A3, D3, w, h, w3, h3, batch);
   oracle_conv_delta(D3, A2, D2, params + off[4], f3, n2, 1, w2, h2, batch);
   oracle_conv_delta(D2, A1, D1, params + off[2], f2, n1, n2, w1, h1, batch);
@@ -349,7 +349,7 @@ void oracle_update_all(int n1, int n2, int f1, int f2, int f3, float* params,
   size_t off[6];
   layer_offsets(n1, n2, f1, f2, f3, off);
   const size_t total = oracle_param_count(n1, n2, f1, f2, f3);
-  /* layer 3, 2, 1 order: ConfigBasedDataPipeline.cpp:491-508 */
+  /* layer 3, 2, 1 order: ConfigBasedDataPipeline.cpp:325-361 */
   for (int l = 2; l >= 0; l--) {
     const size_t wo = off[2 * l], bo = off[2 * l + 1];
     const size_t nW = bo - wo;

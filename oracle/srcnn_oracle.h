@@ -82,7 +82,7 @@ void oracle_swap_luma(const uint8_t* rgba, const float* new_luma,
                       uint8_t* rgb, int w, int h, int luma_w, int luma_h);
 
 /* One reference training chunk: forward L1..L3, last delta, deltas, grads
- * (ConfigBasedDataPipeline.cpp:359-482).  Parameters/grads use the flat
+ * (ConfigBasedDataPipeline.cpp:200-323).  Parameters/grads use the flat
  * layout [W1|B1|W2|B2|W3|B3].  Grads are ACCUMULATED (+=).  Scratch
  * activations are returned in `acts` if non-NULL (A1|A2|A3|D3|D2|D1 per
  * batch, see oracle_train_acts_floats). */
@@ -94,13 +94,13 @@ void oracle_train_fwd_bwd(int n1, int n2, int f1, int f2, int f3,
                           int batch, const float* params, float* grads,
                           float* acts);
 
-/* update all three layers, ConfigBasedDataPipeline.cpp:484-520, then zero
+/* update all three layers, ConfigBasedDataPipeline.cpp:325-361, then zero
  * the gradient accumulators (:511-517). lr[3] per layer. */
 void oracle_update_all(int n1, int n2, int f1, int f2, int f3, float* params,
                        float* grads, float* momentum_bufs, float momentum,
                        float wd, const float* lr, unsigned batch);
 
-/* forward only (inference, ConfigBasedDataPipeline.cpp:273-285 / :359-400),
+/* forward only (inference, ConfigBasedDataPipeline.cpp:114-126 / :200-241),
  * writes A3 [batch][h-pad][w-pad]. */
 void oracle_forward(int n1, int n2, int f1, int f2, int f3, const float* X,
                     int w, int h, int batch, const float* params, float* out);

@@ -150,7 +150,7 @@ def test_swap_luma_spec():
 
 
 def test_train_step_matches_op_composition():
-    """ConfigBasedDataPipeline.cpp:359-520: the orchestrated step equals the
+    """ConfigBasedDataPipeline.cpp:200-361: the orchestrated step equals the
     ops composed by hand, and one update moves params as update_parameters.cl."""
     cfg = (8, 4, 5, 1, 3)
     w = h = 13
