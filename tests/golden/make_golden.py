@@ -9,12 +9,12 @@ inside the test specs.  Nothing here copies reference source code; the
 spec files are read as text and only their number lists are kept.
 
 Sources (all paths relative to /root/reference):
-  test/data/test_cases.json                     LayerTest (test/specs/LayerTest.cpp:13, :97-130)
-  test/specs/LayerDeltasTest.cpp:214-306        input_x / weights / deltas / expected_output
-  test/specs/BackpropagationTest.cpp:410-469    input / deltas / expected grad_w (init 1.5) / grad_b
-  test/specs/ExtractLumaTest.cpp:228-233        expected luma of test/data/color_grid.png
-  test/specs/SwapLumaTest.cpp:305-308           color_grid2.jpg -> color_grid2_luma_swapped.png, padding 10
-  test/data/config*.json                        ConfigTest (test/specs/ConfigTest.cpp:406-422)
+  test/data/test_cases.json                     LayerTest (test/specs/LayerTest.cpp:13)
+  test/specs/LayerDeltasTest.cpp:33-125         input_x / weights / deltas / expected_output
+  test/specs/BackpropagationTest.cpp:31-90       input / deltas / expected grad_w (init 1.5) / grad_b
+  test/specs/ExtractLumaTest.cpp:24-28          expected luma of test/data/color_grid.png
+  test/specs/SwapLumaTest.cpp:21-24            color_grid2.jpg -> color_grid2_luma_swapped.png, padding 10
+  test/data/config*.json                        ConfigTest (test/specs/ConfigTest.cpp:26-45)
 
 Images are decoded with PIL here (the reference decodes with stb_image
 v2.06; PNG decode is lossless so both agree; JPEG decode can differ by a
@@ -80,7 +80,7 @@ def main():
 
     src = read("test/specs/LayerDeltasTest.cpp")
     deltas_fx = {
-        "source": "test/specs/LayerDeltasTest.cpp:214-306,326-368",
+        "source": "test/specs/LayerDeltasTest.cpp:33-125",
         "n_prev_layer": 2, "n_next": 3, "f_next": 3, "curr_w": 5, "curr_h": 5,
         "next_w": 3, "next_h": 3,
         "input_x": array_literal(src, r"float input_x\[INPUT_SIZE\]\s*="),
@@ -94,7 +94,7 @@ def main():
 
     src = read("test/specs/BackpropagationTest.cpp")
     bp = {
-        "source": "test/specs/BackpropagationTest.cpp:410-469,488-533",
+        "source": "test/specs/BackpropagationTest.cpp:31-90",
         "n_prev": 2, "n_cur": 3, "f": 3, "in_w": 5, "in_h": 5,
         "grad_w_init": 1.5,
         "input": array_literal(src, r"float input\[INPUT_SIZE\]\s*="),
@@ -110,7 +110,7 @@ def main():
     src = read("test/specs/ExtractLumaTest.cpp")
     img = Image.open(os.path.join(REF, "test/data/color_grid.png")).convert("RGBA")
     el = {
-        "source": "test/specs/ExtractLumaTest.cpp:228-233, test/data/color_grid.png",
+        "source": "test/specs/ExtractLumaTest.cpp:24-28, test/data/color_grid.png",
         "w": img.size[0], "h": img.size[1],
         "rgba": list(img.tobytes()),
         "expected_normalized": array_literal(src, r"std::vector<float> output\s*="),
@@ -121,7 +121,7 @@ def main():
     src_img = Image.open(os.path.join(REF, "test/data/color_grid2.jpg")).convert("RGBA")
     exp_img = Image.open(os.path.join(REF, "test/data/color_grid2_luma_swapped.png")).convert("RGBA")
     sl = {
-        "source": "test/specs/SwapLumaTest.cpp:305-372, test/data/color_grid2.jpg, "
+        "source": "test/specs/SwapLumaTest.cpp:21-24, test/data/color_grid2.jpg, "
                   "test/data/color_grid2_luma_swapped.png",
         "note": "input JPEG decoded by PIL, the reference decodes with stb_image "
                 "v2.06: a few channels differ by <=2 LSB, so exact parity is "

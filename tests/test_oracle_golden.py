@@ -3,7 +3,7 @@
 Every fixture comes from the reference test suite (tests/golden/make_golden.py
 lists the source file:line of each).  Tolerances follow the precision the
 reference printed its expected values with (3 or 4 decimals), NOT the
-reference's one-sided compare (test/TestCase.cpp:123-138): every check here
+reference's one-sided compare (test/TestCase.cpp:48-62): every check here
 is two-sided.
 """
 import json
@@ -33,7 +33,7 @@ def test_layer_forward_test_cases(case):
 
 
 def test_layer_deltas_spec():
-    """test/specs/LayerDeltasTest.cpp:322-368: prev output = relu(input_x)."""
+    """test/specs/LayerDeltasTest.cpp:141-193: prev output = relu(input_x)."""
     d = load("layer_deltas.json")
     y = np.maximum(np.array(d["input_x"], np.float32), 0)
     out = orc.conv_delta(d["deltas"], y, d["weights"], d["f_next"], d["n_prev_layer"], d["n_next"],
@@ -42,7 +42,7 @@ def test_layer_deltas_spec():
 
 
 def test_backpropagation_spec():
-    """test/specs/BackpropagationTest.cpp:514-533: grad_w init 1.5, grad_b init 0."""
+    """test/specs/BackpropagationTest.cpp:135-159: grad_w init 1.5, grad_b init 0."""
     d = load("backprop.json")
     gW0 = np.full(54, d["grad_w_init"], np.float32)
     gB0 = np.zeros(3, np.float32)
@@ -54,7 +54,7 @@ def test_backpropagation_spec():
 
 
 def test_update_parameters_spec():
-    """test/specs/UpdateParametersTest.cpp:216-296 (fixed seed instead of the clock)."""
+    """test/specs/UpdateParametersTest.cpp:65-105 (fixed seed instead of the clock)."""
     rng = np.random.default_rng(1234)
     n_prev, n_cur, f, batch = 2, 400, 5, 2
     momentum, lr = np.float32(0.8), np.float32(0.001)
@@ -70,7 +70,7 @@ def test_update_parameters_spec():
 
 
 def test_last_layer_delta_spec():
-    """test/specs/LastLayerDeltaTest.cpp:338-386: 6x6 algo result, padding 4."""
+    """test/specs/LastLayerDeltaTest.cpp:34-83: 6x6 algo result, padding 4."""
     rng = np.random.default_rng(7)
     algo_w = algo_h = 6
     pad = 4
@@ -106,7 +106,7 @@ def test_squared_error_spec():
 
 @pytest.mark.parametrize("squared", [False, True])
 def test_sum_spec(squared):
-    """test/specs/SumTest.cpp:114-145: 0..899, margin 20 (:134; the float result
+    """test/specs/SumTest.cpp:27-58: 0..899, margin 20 (:47; the float result
     cannot hold 242595150 exactly)."""
     data = np.arange(900, dtype=np.float32)
     expected = sum(i * i if squared else i for i in range(900))
@@ -114,16 +114,16 @@ def test_sum_spec(squared):
 
 
 def test_subtract_from_all_spec():
-    """test/specs/SubtractFromAllTest.cpp:177-200."""
+    """test/specs/SubtractFromAllTest.cpp:27-50."""
     data = np.arange(900, dtype=np.float32)
     np.testing.assert_array_equal(orc.sub_from_all(data, 450.0), data - 450.0)
 
 
 @pytest.mark.parametrize("normalize", [True, False])
 def test_extract_luma_spec(normalize):
-    """test/specs/ExtractLumaTest.cpp:255-279 on test/data/color_grid.png.
+    """test/specs/ExtractLumaTest.cpp:50-74 on test/data/color_grid.png.
     The spec's expected values are hand-typed to 3 decimals and one of them is
-    3.8e-3 off; the tolerance is the spec's own margin 0.005 (TestCase.cpp:126)."""
+    3.8e-3 off; the tolerance is the spec's own margin 0.005 (TestCase.cpp:51)."""
     d = load("extract_luma.json")
     exp = np.array(d["expected_normalized"], np.float32)
     if not normalize:
@@ -133,7 +133,7 @@ def test_extract_luma_spec(normalize):
 
 
 def test_swap_luma_spec():
-    """test/specs/SwapLumaTest.cpp:323-372.  The reference decodes the input
+    """test/specs/SwapLumaTest.cpp:39-90.  The reference decodes the input
     JPEG with stb_image, the fixture with PIL: 55 of 3072 channels differ by
     1 LSB outside the luma area (pure decoder difference) and 5 by 2 LSB
     inside it, so parity is bounded by 2 LSB on <=2.5% of the channels."""

@@ -91,7 +91,7 @@ def test_backpropagation_spec(S, path):
 
 
 def test_backpropagation_big_data(S, path):
-    """BackpropagationTest.cpp:534-546 (1024x1024, 32->16, f=3): crash-only in
+    """BackpropagationTest.cpp:160-170 (1024x1024, 32->16, f=3): crash-only in
     the reference; here checked against the oracle on random data."""
     rng = np.random.default_rng(11)
     n_prev, n_cur, f, iw = 32, 16, 3, 1024
@@ -178,7 +178,7 @@ def test_sum_spec(S, squared):
     nb = S.reduce_workspace_bytes(900)
     ws, res = zeros(nb // 4 + 1), zeros(1)
     S.buf_sum(D(data), 900, squared, res, ws, nb)
-    assert abs(float(H(res)[0]) - expected) <= 20  # SumTest.cpp:134
+    assert abs(float(H(res)[0]) - expected) <= 20  # SumTest.cpp:47
 
 
 def test_subtract_from_all_and_mean(S):
