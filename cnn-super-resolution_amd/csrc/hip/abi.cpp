@@ -326,7 +326,7 @@ int srcnn_update_all(const srcnn_net* net, float* params, float* grads, float* m
                               (uint32_t)(bo - wo), (uint32_t)(end - bo), stream);
     if (rc) return rc;
   }
-  return srcnn::fill(grads, 0.0f, total, srcnn::as_stream(stream));  // :511-517
+  return srcnn::fill(grads, 0.0f, total, srcnn::as_stream(stream));  // :353-358
 }
 
 size_t srcnn_forward_workspace_bytes(const srcnn_net* net, uint32_t w, uint32_t h,

@@ -1,0 +1,380 @@
+#include "ConfigBasedDataPipeline.hpp"
+
+#include <chrono>
+#include <fstream>
+#include <iostream>
+#include <random>
+#include <string>
+
+#include "Image.hpp"
+#include "Json.hpp"
+
+namespace cnn_sr {
+
+using srcnn::check;
+using srcnn::require;
+
+namespace {
+const char* const kLayerKeys[3] = {"layer1", "layer2", "layer3"};
+}
+
+ConfigBasedDataPipeline::ConfigBasedDataPipeline(Config& cfg, srcnn::Context* ctx)
+    : DataPipeline(ctx),
+      _config(&cfg),
+      layer_data_1(1, cfg.n1, cfg.f1),
+      layer_data_2(cfg.n1, cfg.n2, cfg.f2),
+      layer_data_3(cfg.n2, 1, cfg.f3) {}
+
+srcnn_net ConfigBasedDataPipeline::net() const {
+  srcnn_net n;
+  n.n1 = uint32_t(_config->n1);
+  n.n2 = uint32_t(_config->n2);
+  n.f1 = uint32_t(_config->f1);
+  n.f2 = uint32_t(_config->f2);
+  n.f3 = uint32_t(_config->f3);
+  return n;
+}
+
+void ConfigBasedDataPipeline::init(int load_flags) {
+  DataPipeline::init(load_flags);
+  if (!_config->parameters_file.empty()) {
+    std::cout << "Loading layer parameters from: '" << _config->parameters_file << "'" << std::endl;
+    _epochs = load_parameters_file(_config->parameters_file.c_str());
+    std::cout << "Previous epochs:  " << _epochs << std::endl;
+  } else {
+    std::cout << "No parameters file provided, initializing random weights and biases" << std::endl;
+    uint64_t seed = _seeded ? _seed
+                            : uint64_t(std::chrono::system_clock::now().time_since_epoch().count());
+    fill_random_parameters(layer_data_1, _config->params_distr_1, seed);
+    fill_random_parameters(layer_data_2, _config->params_distr_2, seed + 1);
+    fill_random_parameters(layer_data_3, _config->params_distr_3, seed + 2);
+  }
+  LayerData::validate(layer_data_1);
+  LayerData::validate(layer_data_2);
+  LayerData::validate(layer_data_3);
+}
+
+void ConfigBasedDataPipeline::load_kernels(int load_flags) {
+  DataPipeline::load_kernels(load_flags);
+  using srcnn::KernelKind;
+  if ((load_flags & LOAD_KERNEL_LAYERS) && !_layer_1_kernel) {
+    _layer_1_kernel = create_layer_kernel(layer_data_1, false);
+    _layer_2_kernel = create_layer_kernel(layer_data_2, false);
+    _layer_3_kernel = create_layer_kernel(layer_data_3, true);
+    _forward_kernel = _context->create_kernel(KernelKind::Layer, "forward(net)");
+  }
+  if ((load_flags & LOAD_KERNEL_BACKPROPAGATE) && !_layer_1_deltas_kernel) {
+    _layer_1_deltas_kernel = create_deltas_kernel(layer_data_1);
+    _layer_2_deltas_kernel = create_deltas_kernel(layer_data_2);
+    _train_kernel = _context->create_kernel(KernelKind::Backprop, "train_fwd_bwd(net)");
+    _update_all_kernel = _context->create_kernel(KernelKind::Update, "update_all(net)");
+  }
+}
+
+void ConfigBasedDataPipeline::set_mini_batch_size(size_t n) {
+  _mini_batch_size = n;
+  std::cout << "mini-batch size: " << _mini_batch_size << std::endl;
+}
+
+void ConfigBasedDataPipeline::allocate_buffers(size_t w, size_t h) {
+  if (_out_1_gpu_buf != gpu_nullptr && _buf_w == w && _buf_h == h && _buf_n >= _mini_batch_size)
+    return;
+  _context->block();
+  for (MemoryHandle* m : {&_ground_truth_gpu_buf, &_forward_gpu_buf, &_out_1_gpu_buf, &_out_2_gpu_buf,
+                          &_out_3_gpu_buf, &_delta_1_gpu_buf, &_delta_2_gpu_buf, &_delta_3_gpu_buf}) {
+    if (*m != gpu_nullptr) _context->raw_memory(*m)->release();
+    *m = gpu_nullptr;
+  }
+  size_t d1[2], d2[2], d3[2];
+  layer_data_1.get_output_dimensions(d1, w, h);
+  layer_data_2.get_output_dimensions(d2, d1[0], d1[1]);
+  layer_data_3.get_output_dimensions(d3, d2[0], d2[1]);
+  size_t n = _mini_batch_size * sizeof(float);
+  size_t p0 = w * h, p1 = d1[0] * d1[1] * layer_data_1.current_filter_count,
+         p2 = d2[0] * d2[1] * layer_data_2.current_filter_count,
+         p3 = d3[0] * d3[1] * layer_data_3.current_filter_count;
+  auto rw = srcnn::MEM_READ_WRITE;
+  _ground_truth_gpu_buf = _context->allocate(rw, n * p0);
+  _forward_gpu_buf = _context->allocate(rw, n * p0);
+  _out_1_gpu_buf = _context->allocate(rw, n * p1);
+  _out_2_gpu_buf = _context->allocate(rw, n * p2);
+  _out_3_gpu_buf = _context->allocate(rw, n * p3);
+  _delta_1_gpu_buf = _context->allocate(rw, n * p1);
+  _delta_2_gpu_buf = _context->allocate(rw, n * p2);
+  _delta_3_gpu_buf = _context->allocate(rw, n * p3);
+  _buf_w = w;
+  _buf_h = h;
+  _buf_n = _mini_batch_size;
+}
+
+bool ConfigBasedDataPipeline::bind_flat(LayerAllocationPool& l1, LayerAllocationPool& l2,
+                                        LayerAllocationPool& l3) {
+  LayerAllocationPool* pools[3] = {&l1, &l2, &l3};
+  auto handles = [](const LayerAllocationPool& p) {
+    return std::vector<MemoryHandle>{p.weights, p.bias, p.accumulating_grad_w, p.accumulating_grad_b,
+                                     p.previous_batch_delta_w, p.previous_batch_delta_b};
+  };
+  if (_flat_params != gpu_nullptr) {
+    bool ours = true;
+    for (int i = 0; i < 3; ++i) ours = ours && handles(*pools[i]) == handles(_views[i]);
+    if (ours) return true;
+  }
+  for (int i = 0; i < 3; ++i)
+    for (MemoryHandle m : handles(*pools[i]))
+      if (m != gpu_nullptr) return false;  // caller-owned pools: op-level path
+
+  if (_flat_params == gpu_nullptr) {
+    srcnn_net nt = net();
+    size_t P = srcnn_net_param_count(&nt), off[6];
+    check(srcnn_net_offsets(&nt, off), "srcnn_net_offsets");
+    const LayerData* layers[3] = {&layer_data_1, &layer_data_2, &layer_data_3};
+    std::vector<float> host(P);
+    for (int i = 0; i < 3; ++i) {
+      LayerData::validate(*layers[i]);
+      std::copy(layers[i]->weights.begin(), layers[i]->weights.begin() + layers[i]->weight_size(),
+                host.begin() + off[2 * i]);
+      std::copy(layers[i]->bias.begin(), layers[i]->bias.begin() + layers[i]->bias_size(),
+                host.begin() + off[2 * i + 1]);
+    }
+    auto rw = srcnn::MEM_READ_WRITE;
+    _flat_params = _context->allocate(rw, P * sizeof(float));
+    _flat_grads = _context->allocate(rw, P * sizeof(float));
+    _flat_moms = _context->allocate(rw, P * sizeof(float));
+    _context->write_buffer(_flat_params, host.data(), true);
+    _context->zeros_float(_flat_grads, false);
+    _context->zeros_float(_flat_moms, false);
+    for (int i = 0; i < 3; ++i) {
+      size_t wb = layers[i]->weight_size() * sizeof(float), bb = layers[i]->bias_size() * sizeof(float);
+      size_t wo = off[2 * i] * sizeof(float), bo = off[2 * i + 1] * sizeof(float);
+      _views[i].weights = _context->view(_flat_params, wo, wb);
+      _views[i].bias = _context->view(_flat_params, bo, bb);
+      _views[i].accumulating_grad_w = _context->view(_flat_grads, wo, wb);
+      _views[i].accumulating_grad_b = _context->view(_flat_grads, bo, bb);
+      _views[i].previous_batch_delta_w = _context->view(_flat_moms, wo, wb);
+      _views[i].previous_batch_delta_b = _context->view(_flat_moms, bo, bb);
+    }
+  }
+  for (int i = 0; i < 3; ++i) *pools[i] = _views[i];
+  return true;
+}
+
+// ---------------------------------------------------------------- forward
+
+Event ConfigBasedDataPipeline::forward(LayerAllocationPool& l1, LayerAllocationPool& l2,
+                                       LayerAllocationPool& l3, SampleAllocationPool& sample) {
+  set_mini_batch_size(1);
+  allocate_buffers(sample.input_w, sample.input_h);
+  require(sample.input_luma != gpu_nullptr, "sample has no input luma");
+  _context->copy_buffer(sample.input_luma, _forward_gpu_buf);
+  return forward(l1, l2, l3, sample.input_w, sample.input_h, 1);
+}
+
+Event ConfigBasedDataPipeline::forward(LayerAllocationPool& l1, LayerAllocationPool& l2,
+                                       LayerAllocationPool& l3, size_t w, size_t h, size_t n) {
+  check_initialized(LOAD_KERNEL_LAYERS);
+  if (n > _mini_batch_size) throw std::runtime_error("Allocation pool out of bounds exception");
+  if (bind_flat(l1, l2, l3)) {
+    srcnn_net nt = net();
+    size_t ws = srcnn_forward_workspace_bytes(&nt, w, h, n);
+    void* wsp = scratch(ws);
+    srcnn::Context::Launch l(*_context, *_forward_kernel);
+    check(srcnn_forward(&nt, _context->fptr(_forward_gpu_buf), w, h, n, _context->fptr(_flat_params),
+                        _context->fptr(_out_3_gpu_buf), wsp, ws, _context->stream()),
+          "forward");
+    return _context->mark();
+  }
+  size_t d1[2], d2[2];
+  layer_data_1.get_output_dimensions(d1, w, h);
+  layer_data_2.get_output_dimensions(d2, d1[0], d1[1]);
+  Event e1 = execute_layer(*_layer_1_kernel, layer_data_1, l1, _forward_gpu_buf, w, h, n, _out_1_gpu_buf);
+  Event e2 = execute_layer(*_layer_2_kernel, layer_data_2, l2, _out_1_gpu_buf, d1[0], d1[1], n,
+                           _out_2_gpu_buf, &e1);
+  return execute_layer(*_layer_3_kernel, layer_data_3, l3, _out_2_gpu_buf, d2[0], d2[1], n,
+                       _out_3_gpu_buf, &e2);
+}
+
+// ---------------------------------------------------------------- training
+
+Event ConfigBasedDataPipeline::backpropagate(LayerAllocationPool& l1, LayerAllocationPool& l2,
+                                             LayerAllocationPool& l3, size_t w, size_t h, size_t n,
+                                             Event* ev) {
+  size_t d1[2], d2[2], d3[2];
+  layer_data_1.get_output_dimensions(d1, w, h);
+  layer_data_2.get_output_dimensions(d2, d1[0], d1[1]);
+  layer_data_3.get_output_dimensions(d3, d2[0], d2[1]);
+  size_t pad = _config->total_padding();
+  Event e = last_layer_delta(_ground_truth_gpu_buf, w, h, n, _out_3_gpu_buf, _delta_3_gpu_buf, pad, ev);
+  e = calculate_deltas(*_layer_2_deltas_kernel, layer_data_2, layer_data_3, l3, _delta_2_gpu_buf,
+                       _delta_3_gpu_buf, d3[0], d3[1], n, _out_2_gpu_buf, &e);
+  e = calculate_deltas(*_layer_1_deltas_kernel, layer_data_1, layer_data_2, l2, _delta_1_gpu_buf,
+                       _delta_2_gpu_buf, d2[0], d2[1], n, _out_1_gpu_buf, &e);
+  DataPipeline::backpropagate(layer_data_3, _out_2_gpu_buf, _delta_3_gpu_buf, l3, d3[0], d3[1], n, &e);
+  DataPipeline::backpropagate(layer_data_2, _out_1_gpu_buf, _delta_2_gpu_buf, l2, d2[0], d2[1], n, &e);
+  return DataPipeline::backpropagate(layer_data_1, _forward_gpu_buf, _delta_1_gpu_buf, l1, d1[0],
+                                     d1[1], n, &e);
+}
+
+float ConfigBasedDataPipeline::execute_batch(bool backprop, GpuAllocationPool& gpu_alloc,
+                                             std::vector<SampleAllocationPool*>& samples) {
+  if (samples.empty() || _mini_batch_size == 0) throw std::runtime_error("Batch cannot be empty");
+  check_initialized(backprop ? (LOAD_KERNEL_LAYERS | LOAD_KERNEL_BACKPROPAGATE)
+                             : (LOAD_KERNEL_LAYERS | LOAD_KERNEL_MISC));
+  size_t w = samples[0]->input_w, h = samples[0]->input_h;
+  for (auto* s : samples) {
+    require(s && s->input_w == w && s->input_h == h, "All samples of a batch must have the same size");
+    require(s->input_luma != gpu_nullptr && s->expected_luma != gpu_nullptr,
+            "Sample without input / expected luma");
+  }
+  allocate_buffers(w, h);
+  LayerAllocationPool &l1 = gpu_alloc.layer_1, &l2 = gpu_alloc.layer_2, &l3 = gpu_alloc.layer_3;
+  bool flat = bind_flat(l1, l2, l3);
+  srcnn_net nt = net();
+  size_t tile_bytes = w * h * sizeof(float);
+  float validation_error = 0.f;
+  for (size_t i = 0; i < samples.size();) {
+    size_t n = 0;
+    for (; n < _mini_batch_size && i + n < samples.size(); ++n) {
+      SampleAllocationPool& s = *samples[i + n];
+      _context->copy_buffer(s.input_luma, _forward_gpu_buf, n * tile_bytes);
+      _context->copy_buffer(s.expected_luma, _ground_truth_gpu_buf, n * tile_bytes);
+    }
+    if (backprop && flat) {
+      size_t ws = srcnn_train_workspace_bytes(&nt, w, h, n);
+      void* wsp = scratch(ws);
+      srcnn::Context::Launch l(*_context, *_train_kernel);
+      check(srcnn_train_fwd_bwd(&nt, _context->fptr(_forward_gpu_buf), _context->fptr(_ground_truth_gpu_buf),
+                                w, h, n, _context->fptr(_flat_params), _context->fptr(_flat_grads),
+                                nullptr, wsp, ws, _context->stream()),
+            "execute_batch");
+    } else if (backprop) {
+      Event e = forward(l1, l2, l3, w, h, n);
+      backpropagate(l1, l2, l3, w, h, n, &e);
+    } else {
+      Event e = forward(l1, l2, l3, w, h, n);
+      float err = 0.f;
+      squared_error(_ground_truth_gpu_buf, w, h, n, _out_3_gpu_buf, gpu_nullptr, err,
+                    _config->total_padding(), &e);
+      validation_error += err;
+    }
+    _context->block();
+    i += n;
+  }
+  return validation_error;
+}
+
+void ConfigBasedDataPipeline::update_parameters(LayerAllocationPool& l1, LayerAllocationPool& l2,
+                                                LayerAllocationPool& l3, size_t batch, Event* ev) {
+  check_initialized(LOAD_KERNEL_BACKPROPAGATE);
+  bool flat = _flat_params != gpu_nullptr;
+  LayerAllocationPool* pools[3] = {&l1, &l2, &l3};
+  for (int i = 0; flat && i < 3; ++i)
+    flat = pools[i]->weights == _views[i].weights && pools[i]->accumulating_grad_w == _views[i].accumulating_grad_w &&
+           pools[i]->previous_batch_delta_w == _views[i].previous_batch_delta_w;
+  if (flat) {
+    _context->wait(ev);
+    srcnn_net nt = net();
+    const float* lr = _config->learning_rate;
+    srcnn::Context::Launch l(*_context, *_update_all_kernel);
+    check(srcnn_update_all(&nt, _context->fptr(_flat_params), _context->fptr(_flat_grads),
+                           _context->fptr(_flat_moms), _config->momentum,
+                           _config->weight_decay_parameter, lr, uint32_t(batch), _context->stream()),
+          "update_parameters");
+  } else {
+    DataPipeline::update_parameters(layer_data_3, l3, batch, _config->momentum,
+                                    _config->weight_decay_parameter, _config->learning_rate[2], ev);
+    DataPipeline::update_parameters(layer_data_2, l2, batch, _config->momentum,
+                                    _config->weight_decay_parameter, _config->learning_rate[1], ev);
+    DataPipeline::update_parameters(layer_data_1, l1, batch, _config->momentum,
+                                    _config->weight_decay_parameter, _config->learning_rate[0], ev);
+    for (auto* p : pools) {
+      _context->zeros_float(p->accumulating_grad_w, false);
+      _context->zeros_float(p->accumulating_grad_b, false);
+    }
+  }
+  _context->block();
+  ++_epochs;
+}
+
+// ---------------------------------------------------------------- parameters I/O
+
+void ConfigBasedDataPipeline::fill_random_parameters(LayerData& d, ParametersDistribution& pd,
+                                                     uint64_t seed) {
+  std::mt19937_64 gen(seed);
+  auto draw = [&gen](float mean, float sd) {
+    if (!(sd > 0.f)) return mean;
+    std::normal_distribution<float> dist(mean, sd);
+    return dist(gen);
+  };
+  d.weights.clear();
+  d.bias.clear();
+  for (size_t i = 0; i < d.weight_size(); ++i) d.weights.push_back(draw(pd.mean_w, pd.sd_w));
+  for (size_t i = 0; i < d.bias_size(); ++i) d.bias.push_back(draw(pd.mean_b, pd.sd_b));
+}
+
+size_t ConfigBasedDataPipeline::load_parameters_file(const char* file) {
+  using namespace srcnn::json;
+  Value root = parse_file(file, Tag::Object);
+  size_t epochs = 0;
+  LayerData* layers[3] = {&layer_data_1, &layer_data_2, &layer_data_3};
+  for (auto& kv : root.object) {
+    if (try_read_uint(kv.first, kv.second, epochs, "epochs")) continue;
+    bool known = false;
+    for (int i = 0; i < 3; ++i) {
+      if (kv.first != kLayerKeys[i]) continue;
+      known = true;
+      for (auto& sub : kv.second.object) {
+        try_read_vector(sub.first, sub.second, layers[i]->weights, "weights");
+        try_read_vector(sub.first, sub.second, layers[i]->bias, "bias");
+      }
+    }
+    if (!known) std::cout << "[Warning] Unknown key '" << kv.first << "' in parameters file" << std::endl;
+  }
+  return epochs;
+}
+
+void ConfigBasedDataPipeline::write_params_to_file(const char* path, LayerAllocationPool l1,
+                                                   LayerAllocationPool l2, LayerAllocationPool l3) {
+  std::cout << "Saving parameters to: '" << path << "'" << std::endl;
+  LayerData* layers[3] = {&layer_data_1, &layer_data_2, &layer_data_3};
+  LayerAllocationPool* pools[3] = {&l1, &l2, &l3};
+  _context->block();
+  for (int i = 0; i < 3; ++i) {
+    LayerData& d = *layers[i];
+    d.weights.resize(d.weight_size());
+    d.bias.resize(d.bias_size());
+    if (pools[i]->weights != gpu_nullptr)
+      _context->read_buffer(pools[i]->weights, 0, d.weight_size() * sizeof(float), d.weights.data(), true);
+    if (pools[i]->bias != gpu_nullptr)
+      _context->read_buffer(pools[i]->bias, 0, d.bias_size() * sizeof(float), d.bias.data(), true);
+  }
+  std::ofstream out(path);
+  if (!out.is_open()) throw srcnn::IOException(std::string("Could not write parameters file: ") + path);
+  auto dump = [&out](const std::vector<float>& v) {
+    for (size_t i = 0; i < v.size(); ++i) out << (i ? ", " : "") << srcnn::json::format_float(v[i]);
+  };
+  out << "{\n  \"epochs\": " << _epochs << ",\n\n";
+  for (int i = 0; i < 3; ++i) {
+    out << "  \"" << kLayerKeys[i] << "\":{\n    \"weights\": [";
+    dump(layers[i]->weights);
+    out << "],\n    \"bias\": [";
+    dump(layers[i]->bias);
+    out << "]\n  }" << (i < 2 ? ",\n" : "\n");
+  }
+  out << "}";
+}
+
+void ConfigBasedDataPipeline::write_result_image(const char* out_path, ImageData& img,
+                                                 SampleAllocationPool& sample) {
+  std::cout << "Saving result image to: '" << out_path << "'" << std::endl;
+  size_t pad = _config->total_padding();
+  require(size_t(img.w) > pad && size_t(img.h) > pad, "image smaller than the network padding");
+  size_t lw = img.w - pad, lh = img.h - pad;
+  MemoryHandle target = gpu_nullptr;
+  swap_luma(img, sample.input_data, _out_3_gpu_buf, target, lw, lh);
+  ImageData res(img.w, img.h, 3);
+  _context->read_buffer(target, 0, res.data.size(), res.data.data(), true);
+  _context->raw_memory(target)->release();
+  srcnn::image::write(out_path, res);
+}
+
+}  // namespace cnn_sr

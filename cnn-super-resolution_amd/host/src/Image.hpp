@@ -1,0 +1,35 @@
+// Image files for the `cnn` CLI and the luma helpers.
+//
+// The reference reads/writes images with the vendored stb_image /
+// stb_image_write (src/opencl/UtilsOpenCL.cpp load_image / write_image).
+// This is an independent codec set built on the system zlib:
+//   PNG  read: 8-bit gray / gray+alpha / RGB / RGBA / palette, non-interlaced;
+//        write: 8-bit gray, RGB or RGBA
+//   PNM  read/write: binary P5 (gray) / P6 (RGB)
+// JPEG is not decoded here (no decoder in the image's toolchain): convert
+// JPEG samples to PNG first (tools/make_samples.py does).
+#ifndef SRCNN_HOST_IMAGE_HPP
+#define SRCNN_HOST_IMAGE_HPP
+
+#include <string>
+
+#include "Context.hpp"
+
+namespace srcnn {
+namespace image {
+
+/** Load a PNG or PNM file (by content) into `img`; `channels` 0 keeps the
+ * file's channel count, 1/3/4 converts (gray <-> RGB, alpha = 255). */
+void load(const std::string& path, ImageData& img, int channels = 0);
+
+/** Write `img` (bpp 1, 3 or 4) as PNG, or PNM when the path ends in
+ * .pgm/.ppm/.pnm (RGBA written as RGB there). */
+void write(const std::string& path, const ImageData& img);
+
+/** Write a float luma plane (values in [0,1], clamped) as an 8-bit gray PNG. */
+void write_luma(const std::string& path, const float* luma, int w, int h);
+
+}  // namespace image
+}  // namespace srcnn
+
+#endif  // SRCNN_HOST_IMAGE_HPP

@@ -63,7 +63,7 @@ SRCNN_API int srcnn_memcpy_h2d(void* dst, const void* src, size_t bytes, srcnn_s
 SRCNN_API int srcnn_memcpy_d2h(void* dst, const void* src, size_t bytes, srcnn_stream_t stream);
 /* async D2D (copy_buffer, Context.cpp:312-341) */
 SRCNN_API int srcnn_memcpy_d2d(void* dst, const void* src, size_t bytes, srcnn_stream_t stream);
-/* async fill (zeros_float / fill_float, Context.cpp:292-310; no host vector) */
+/* async fill (zeros_float / fill_float, Context.cpp:296-310; no host vector) */
 SRCNN_API int srcnn_fill_f32(float* dst, float value, size_t count, srcnn_stream_t stream);
 SRCNN_API int srcnn_stream_create(srcnn_stream_t* stream);
 SRCNN_API int srcnn_stream_destroy(srcnn_stream_t stream);

@@ -62,8 +62,8 @@ def test_update_parameters_spec():
         cur = (rng.integers(0, 2560, size) / 10.0).astype(np.float32)
         grad = (rng.integers(0, 2560, size) / 100.0).astype(np.float32)
         prev = (rng.integers(0, 2560, size) / 10.0).astype(np.float32)
-        deltas = momentum * prev + lr * grad                       # :229
-        expected = cur - deltas / np.float32(batch)                 # :230
+        deltas = momentum * prev + lr * grad                       # :35
+        expected = cur - deltas / np.float32(batch)                 # :36
         W, B, dW, dB = orc.sgd_update(cur, cur[:1], grad, grad[:1], prev, prev[:1], 0.8, 0.0, 0.001, batch)
         np.testing.assert_allclose(W, expected, rtol=1e-6, atol=1e-4)
         np.testing.assert_allclose(dW, deltas, rtol=1e-6, atol=1e-4)
@@ -83,7 +83,7 @@ def test_last_layer_delta_spec():
         t = np.float32(rng.integers(0, 256) / 100.0)
         x = np.float32(rng.integers(0, 2560) / 1000.0) - np.float32(1.28)   # both ReLU branches
         y = max(x, np.float32(0))
-        exp[i] = (y - t) * (1.0 if x > 0 else 0.0)                          # :368
+        exp[i] = (y - t) * (1.0 if x > 0 else 0.0)                          # :64
         gt[(r + pad) * gw + pad + c] = t
         algo[i] = y
     out = orc.last_delta(gt, algo, gw, gh, algo_w, algo_h, 1)
@@ -140,7 +140,7 @@ def test_swap_luma_spec():
     d = load("swap_luma.json")
     w, h, pad = d["w"], d["h"], d["padding"]
     lw, lh = w - 2 * pad, h - 2 * pad
-    n = lw * lw                                              # :332 (luma_w * luma_w)
+    n = lw * lw                                              # :48 (luma_w * luma_w)
     new_luma = (np.arange(n, dtype=np.float32) * np.float32(1.0)) / np.float32(n)
     out = orc.swap_luma(np.array(d["rgba"], np.uint8), new_luma, w, h, lw, lh).astype(int)
     exp = np.array(d["expected_rgba"], np.uint8).reshape(-1, 4)[:, :3].reshape(-1).astype(int)
