@@ -1,6 +1,6 @@
 // l3_delta.hpp -- fused kernel 2 of train_fused.hip (included inside
 // namespace srcnn::fused): per sample, with the A2 tile resident in LDS,
-//   L3 forward       layer_uber_kernel.cl:70-91 (SKIP_RELU), VALU
+//   L3 forward       layer_uber_kernel.cl:70-91 (SKIP_RELU)
 //   last delta       last_layer_delta.cl:34-48 (relu' quirk on a linear layer)
 //   squared error    squared_error.cl:60-69 (validation metric)
 //   delta2           layer_deltas.cl:79-123, MFMA over the f3*f3 taps
@@ -8,23 +8,53 @@
 // 8 waves per block, one block per CU; the next sample's A2 tile is
 // prefetched into registers while the current one is processed.
 //
-// L3 mapping: 8 lanes per output segment, lane c4 owns channels 4c4..4c4+3
-// of a 1x4 run of outputs; the 8 channel-group partials are combined with
-// lane shuffles.  W3 lives in LDS (read as float4).
+// L3 forward has one output channel, so it is not a GEMM as written.  It is
+// split into a GEMM and a gather ("Q trick"):
+//   Q[q][tap] = sum_c A2[q][c] * W3[tap][c]        (MFMA, M = pixels, N = taps, K = channels)
+//   A3[p]     = B3 + sum_tap Q[p + off(tap)][tap]  (25 LDS reads per output)
+// which moves the 5x5x32 window sums from LDS-bound VALU onto the matrix
+// cores.  Q lives in LDS next to the A2 tile (stride K3: conflict-free reads).
+//
+// A2 LDS image: rows of N2 floats, 16-byte quads XOR-swizzled by row
+// (quad q of row p at q ^ ((p >> 1) & (N2/4 - 1))), so both the per-pixel
+// column reads of the MFMA A operand and the per-channel row reads are
+// (at most 2-way) bank-conflict free without padding.
+#ifdef SRCNN_L3_TIMING
+// diagnostics build only: per-block cycles spent between the phase barriers
+__device__ unsigned long long g_l3_timing[1024][4];
+#define SRCNN_L3_TICK(PH)                                             \
+  do {                                                                \
+    if (threadIdx.x == 0) {                                           \
+      const unsigned long long now_ = clock64();                      \
+      tacc[(PH + 3) & 3] += now_ - tlast;                             \
+      tlast = now_;                                                   \
+    }                                                                 \
+  } while (0)
+#else
+#define SRCNN_L3_TICK(PH) \
+  do {                    \
+  } while (0)
+#endif
+
 struct L3Geom {
   int W, H;     // ground-truth sample (= network input size)
   int w2, h2;   // A2
   int w3, h3;   // A3
   int batch;
-  int ablate;   // diagnostics only (env SRCNN_ABLATE_L3): bit0 L3, bit1 delta2, bit2 gW3
 };
 
 constexpr int kL3Threads = 512;
-constexpr int kL3Seg = 4;  // outputs per L3 work item (one row segment)
 
 template <int N2, int F3>
 __host__ __device__ constexpr int l3_prefetch_regs(int npx2) {
   return (npx2 * (N2 / 4) + kL3Threads - 1) / kL3Threads;
+}
+
+// float index of A2[p][n] in the swizzled LDS image
+template <int N2>
+__device__ __forceinline__ int a2_at(int p, int n) {
+  constexpr int NQ = N2 / 4;
+  return p * N2 + 4 * ((n >> 2) ^ ((p >> 1) & (NQ - 1))) + (n & 3);
 }
 
 template <int N2, int F3, int PF>
@@ -33,32 +63,50 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
     const float* __restrict__ B3, float* __restrict__ D2, float* __restrict__ slab3,
     float* __restrict__ sq_slab, L3Geom g) {
   constexpr int K3 = F3 * F3, KS3 = (K3 + 1) / 2, NT2 = (N2 + 31) / 32;
-  constexpr int N2S = N2 + 4;       // padded A2 row
+  constexpr int KC = N2 / 2;        // Q k-steps (over channels)
   constexpr int NW3 = K3 * N2;      // gW3 size; slab row = NW3 + 1 (gB3)
-  constexpr int C4 = N2 / 4;        // channel quads (lanes per L3 work item)
-  static_assert(K3 <= 32, "taps must fit one 32-row MFMA tile");
-  static_assert(N2 % 4 == 0 && 64 % C4 == 0, "n2 must be a multiple of 4 dividing 256");
+  constexpr int NQ = N2 / 4;        // quads per A2 row
+  static_assert(K3 <= 32, "taps must fit one 32-wide MFMA tile");
+  static_assert(N2 % 8 == 0 && (NQ & (NQ - 1)) == 0, "n2 must be 8 * 2^k");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int npx2 = g.w2 * g.h2;
-  const int w3p = g.w3 + 2 * (F3 - 1), h3p = g.h3 + 2 * (F3 - 1);
-  float* a2s = smem;                                        // [npx2 + 8][N2S]
-  float* w3s = smem + (((npx2 + 8) * N2S + 3) & ~3);        // [K3][N2]
-  float* d3p = w3s + ((NW3 + 3) & ~3);                      // [h3p][w3p], zero border
-  float* red = d3p + ((w3p * h3p + 3) & ~3);                // [NT2*1024] reduction scratch
+  const int nch = (npx2 + 31) / 32;
+  // delta3 on the A2 grid: delta3(y, x) at d3g[(y + F3-1) * w2 + x + F3-1], zero
+  // elsewhere (w3 = w2 - (F3-1), so a row's F3-1 leading columns are the zero
+  // border of the previous row's wrap).  delta3(y - dy, x - dx) for A2 pixel
+  // p = y*w2 + x is then d3g[p + (F3-1)*(w2+1) - (dy*w2 + dx)]: one add.
+  const int d3off = (F3 - 1) * (g.w2 + 1);
+  const int nd3 = nch * 32 + d3off + 4;
+  float* a2s = smem;                          // [nch*32][N2] swizzled (rows >= npx2 zero)
+  float* qs = a2s + nch * 32 * N2;            // [npx2][K3]
+  float* d3g = qs + ((npx2 * K3 + 3) & ~3);   // [nd3]
+  float* red = qs;                            // end-of-kernel reduction scratch (aliases qs)
 
   const int tid = threadIdx.x;
   const int lane = mfma::lane_id(), wave = mfma::wave_id();
   const int h = lane >> 5, li = lane & 31;
-  const int nwaves = kL3Threads / 64;
+  constexpr int nwaves = kL3Threads / 64;
   const int pad = (g.W - g.w3) / 2;  // last_layer_delta.cl:25
 
-  for (int i = tid; i < w3p * h3p; i += kL3Threads) d3p[i] = 0.0f;
-  for (int i = tid; i < NW3; i += kL3Threads) w3s[i] = W3[i];
-  for (int i = tid; i < 8 * N2S; i += kL3Threads) a2s[npx2 * N2S + i] = 0.0f;  // overrun rows
+  for (int i = tid; i < nd3; i += kL3Threads) d3g[i] = 0.0f;
+  for (int i = npx2 * N2 + tid; i < nch * 32 * N2; i += kL3Threads) a2s[i] = 0.0f;
 
-  // gW3 A-operand row of this lane: tap li
-  const int my_dy = li / F3, my_dx = li - (li / F3) * F3;
+  // B operand of Q: W3[tap = li][c = 2s + h]
+  float wq[KC];
+#pragma unroll
+  for (int s = 0; s < KC; s++) wq[s] = li < K3 ? W3[li * N2 + 2 * s + h] : 0.0f;
+  // B operand of delta2: W3[tap = 2s + h][n = 32u + li]
+  float wd[KS3][NT2];
+#pragma unroll
+  for (int s = 0; s < KS3; s++)
+#pragma unroll
+    for (int u = 0; u < NT2; u++) {
+      const int tap = 2 * s + h, n = 32 * u + li;
+      wd[s][u] = (tap < K3 && n < N2) ? W3[tap * N2 + n] : 0.0f;
+    }
+  // gW3 A-operand row of this lane: tap li -> d3g offset of its window
   const bool my_tap = li < K3;
+  const int my_off = d3off - (my_tap ? (li / F3) * g.w2 + li % F3 : 0);
   const float b3 = B3[0];
 
   f32x16 gacc[NT2];
@@ -68,146 +116,148 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
 
   // register prefetch of one A2 tile: PF float4 per thread
   float4 pf[PF];
-  const int nq = npx2 * C4;
+  const int nq = npx2 * NQ;
 #define SRCNN_L3_PREFETCH(SAMPLE)                                                        \
   do {                                                                                   \
     const float4* src_ = reinterpret_cast<const float4*>(A2 + (size_t)(SAMPLE)*npx2 * N2); \
+    int t_ = tid; /* opaque: addresses are formed at the load, never held (spilled) */   \
+    asm volatile("" : "+v"(t_));                                                         \
     _Pragma("unroll") for (int k = 0; k < PF; k++) {                                     \
-      const int i_ = tid + k * kL3Threads;                                               \
+      const int i_ = t_ + k * kL3Threads;                                                \
       pf[k] = i_ < nq ? src_[i_] : make_float4(0.f, 0.f, 0.f, 0.f);                      \
     }                                                                                    \
   } while (0)
   if ((int)blockIdx.x < g.batch) SRCNN_L3_PREFETCH(blockIdx.x);
 
-  const int nseg = (g.w3 + kL3Seg - 1) / kL3Seg;
-  const int nitems = g.h3 * nseg;
-  const int c4 = tid % C4, item0 = tid / C4;
-  const int items_per_pass = kL3Threads / C4;
+#ifdef SRCNN_L3_TIMING
+  unsigned long long tacc[4] = {0, 0, 0, 0}, tlast = clock64();
+#endif
+  const int nout = g.w3 * g.h3;
+  // ground truth of this thread's L3 outputs, prefetched one sample ahead
+  constexpr int TPF = 2;  // outputs per thread (w3 * h3 <= TPF * 512)
+  float tpf[TPF];
+#define SRCNN_L3_T_PREFETCH(SAMPLE)                                                    \
+  do {                                                                                 \
+    _Pragma("unroll") for (int k = 0; k < TPF; k++) {                                  \
+      const int t_ = tid + k * kL3Threads;                                             \
+      const int y_ = t_ / g.w3, x_ = t_ - (t_ / g.w3) * g.w3;                          \
+      tpf[k] = t_ < nout ? T[(size_t)(SAMPLE)*g.W * g.H + (size_t)(y_ + pad) * g.W + x_ + pad] : 0.f; \
+    }                                                                                  \
+  } while (0)
+  if ((int)blockIdx.x < g.batch) SRCNN_L3_T_PREFETCH(blockIdx.x);
 
   for (int sample = blockIdx.x; sample < g.batch; sample += gridDim.x) {
     __syncthreads();  // previous sample fully consumed a2s / d3p
+    SRCNN_L3_TICK(0);
 #pragma unroll
     for (int k = 0; k < PF; k++) {
       const int i = tid + k * kL3Threads;
       if (i < nq) {
-        const int p = i / C4, q = i - p * C4;
-        *reinterpret_cast<float4*>(a2s + p * N2S + 4 * q) = pf[k];
+        const int p = i / NQ, q = i - p * NQ;
+        *reinterpret_cast<float4*>(a2s + a2_at<N2>(p, 4 * q)) = pf[k];
       }
     }
-    if (sample + (int)gridDim.x < g.batch) SRCNN_L3_PREFETCH(sample + gridDim.x);
+    float tcur[TPF];
+#pragma unroll
+    for (int k = 0; k < TPF; k++) tcur[k] = tpf[k];
+    if (sample + (int)gridDim.x < g.batch) {
+      SRCNN_L3_PREFETCH(sample + gridDim.x);
+      SRCNN_L3_T_PREFETCH(sample + gridDim.x);
+    }
     __syncthreads();
+    SRCNN_L3_TICK(1);
 
-    // ---- L3 forward + last delta + squared error ----
-    for (int it = item0; (g.ablate & 1) == 0 && it < nitems; it += items_per_pass) {
-      const int y = it / nseg, x0 = (it - y * nseg) * kL3Seg;
-      float acc[kL3Seg];
+    // ---- Q = A2 . W3^T per 32-pixel chunk ----
+    for (int c = wave; c < nch; c += nwaves) {
+      const int p = c * 32 + li;
+      f32x16 acc = zero16();
 #pragma unroll
-      for (int j = 0; j < kL3Seg; j++) acc[j] = 0.0f;
-#pragma unroll 1
-      for (int dy = 0; dy < F3; dy++) {
-        float4 v[kL3Seg + F3 - 1];
-        const float* row = a2s + ((y + dy) * g.w2 + x0) * N2S + 4 * c4;
+      for (int s = 0; s < KC; s++) acc = mma(a2s[a2_at<N2>(p, 2 * s + h)], wq[s], acc);
+      if (li < K3) {
 #pragma unroll
-        for (int j = 0; j < kL3Seg + F3 - 1; j++) v[j] = *reinterpret_cast<const float4*>(row + j * N2S);
-#pragma unroll
-        for (int dx = 0; dx < F3; dx++) {
-          const float4 w = *reinterpret_cast<const float4*>(w3s + (dy * F3 + dx) * N2 + 4 * c4);
-#pragma unroll
-          for (int j = 0; j < kL3Seg; j++) {
-            const float4 a = v[j + dx];
-            acc[j] += a.x * w.x + a.y * w.y + a.z * w.z + a.w * w.w;
-          }
-        }
-      }
-      // combine the C4 channel-group partials (lanes c4 = 0..C4-1 are adjacent)
-#pragma unroll
-      for (int off = 1; off < C4; off <<= 1)
-#pragma unroll
-        for (int j = 0; j < kL3Seg; j++) acc[j] += __shfl_xor(acc[j], off, 64);
-      if (c4 < kL3Seg) {
-        float mine = acc[0];
-#pragma unroll
-        for (int j = 1; j < kL3Seg; j++) mine = c4 == j ? acc[j] : mine;
-        const int x = x0 + c4;
-        if (x < g.w3) {
-          const float a3 = mine + b3;
-          const float t = T[(size_t)sample * g.W * g.H + (size_t)(y + pad) * g.W + x + pad];
-          const float diff = a3 - t;
-          const float d3 = diff * (a3 > 0.0f ? 1.0f : 0.0f);
-          d3p[(y + F3 - 1) * w3p + x + F3 - 1] = d3;
-          gb3 += d3;
-          sq += diff * diff;
+        for (int r = 0; r < 16; r++) {
+          const int q = c * 32 + crow(r, h);
+          if (q < npx2) qs[q * K3 + li] = acc[r];
         }
       }
     }
     __syncthreads();
+    SRCNN_L3_TICK(2);
 
-    // ---- delta2: per 32-pixel chunk of the A2 grid ----
-    const int nch = (npx2 + 31) / 32;
-    for (int c = wave; (g.ablate & 2) == 0 && c < nch; c += nwaves) {
-      const int p = min(c * 32 + li, npx2 - 1);
-      const int y = p / g.w2, x = p - y * g.w2;
-      const int base = (y + F3 - 1) * w3p + x + F3 - 1;
+    // ---- L3 = B3 + diagonal sums of Q; last delta; squared error ----
+#pragma unroll
+    for (int k = 0; k < TPF; k++) {
+      const int t = tid + k * kL3Threads;
+      if (t < nout) {
+        const int y = t / g.w3, x = t - y * g.w3;
+        const float* qrow = qs + (y * g.w2 + x) * K3;
+        float acc = 0.0f;
+#pragma unroll
+        for (int dy = 0; dy < F3; dy++)
+#pragma unroll
+          for (int dx = 0; dx < F3; dx++) acc += qrow[(dy * g.w2 + dx) * K3 + dy * F3 + dx];
+        const float a3 = acc + b3;
+        const float diff = a3 - tcur[k];
+        const float d3 = diff * (a3 > 0.0f ? 1.0f : 0.0f);
+        d3g[y * g.w2 + x + d3off] = d3;
+        gb3 += d3;
+        sq += diff * diff;
+      }
+    }
+    __syncthreads();
+    SRCNN_L3_TICK(3);
+
+    // ---- per 32-pixel chunk: delta2 (MFMA over taps) and gW3 (MFMA over pixels) ----
+    for (int c = wave; c < nch; c += nwaves) {
+      const int c0 = c * 32;
+      // delta2[q][n] = [A2 > 0] * sum_tap delta3(q - off(tap)) W3[tap][n], q = c0 + li
       f32x16 acc[NT2];
 #pragma unroll
       for (int u = 0; u < NT2; u++) acc[u] = zero16();
 #pragma unroll
       for (int s = 0; s < KS3; s++) {
-        const int k0 = 2 * s, k1 = 2 * s + 1;
-        const int o0 = (k0 / F3) * w3p + (k0 % F3);
-        const int o1 = k1 < K3 ? (k1 / F3) * w3p + (k1 % F3) : 0;
-        const float a = d3p[base - (h ? o1 : o0)];
-        const int tap = h ? k1 : k0;
+        const int tap = 2 * s + h;
+        const int o = tap < K3 ? (tap / F3) * g.w2 + tap % F3 : 0;
+        const float a = tap < K3 ? d3g[c0 + li + d3off - o] : 0.0f;
+#pragma unroll
+        for (int u = 0; u < NT2; u++) acc[u] = mma(a, wd[s][u], acc[u]);
+      }
+      // gW3[tap][n] += sum_p delta3(p - off(tap)) A2[p][n], p = c0 + 2s + h
+      // (rows >= npx2 of a2s and the d3g tail are zero: no bounds checks)
+#pragma unroll
+      for (int s = 0; s < 16; s++) {
+        const int p = c0 + 2 * s + h;
+        const float a = my_tap ? d3g[p + my_off] : 0.0f;
 #pragma unroll
         for (int u = 0; u < NT2; u++) {
-          // B operand W3[tap][n = 32u + li] (zero past the taps / channels)
           const int n = 32 * u + li;
-          const float b = (tap < K3 && n < N2) ? w3s[tap * N2 + n] : 0.0f;
-          acc[u] = mma(a, b, acc[u]);
+          gacc[u] = mma(a, n < N2 ? a2s[a2_at<N2>(p, n)] : 0.0f, gacc[u]);
         }
+        if ((s & 7) == 7) __builtin_amdgcn_sched_barrier(0);  // bound the operand hoisting
       }
 #pragma unroll
       for (int r = 0; r < 16; r++) {
-        const int pr = c * 32 + crow(r, h);
+        const int pr = c0 + crow(r, h);
         if (pr < npx2) {
 #pragma unroll
           for (int u = 0; u < NT2; u++) {
             const int n = 32 * u + li;
             if (n < N2) {
-              const float m = a2s[pr * N2S + n] > 0.0f ? 1.0f : 0.0f;
+              const float m = a2s[a2_at<N2>(pr, n)] > 0.0f ? 1.0f : 0.0f;
               D2[((size_t)sample * npx2 + pr) * N2 + n] = acc[u][r] * m;
             }
           }
         }
       }
     }
-
-    // ---- gW3: G[tap][n] += sum_p' d3p[p' - tap] * A2[p'][n] ----
-    {
-      const int nks = (g.ablate & 4) ? 0 : (npx2 + 1) / 2;
-      int pp = 2 * wave + h;
-      int yq = pp / g.w2, xq = pp - yq * g.w2;
-      const int stride = 2 * nwaves;
-      for (int j = wave; j < nks; j += nwaves) {
-        const bool v = pp < npx2;
-        const float a =
-            (v && my_tap) ? d3p[(yq - my_dy + F3 - 1) * w3p + xq - my_dx + F3 - 1] : 0.0f;
-#pragma unroll
-        for (int u = 0; u < NT2; u++) {
-          const int n = 32 * u + li;
-          const float b = (v && n < N2) ? a2s[pp * N2S + n] : 0.0f;
-          gacc[u] = mma(a, b, gacc[u]);
-        }
-        pp += stride;
-        xq += stride;
-        while (xq >= g.w2) {
-          xq -= g.w2;
-          yq++;
-        }
-      }
-    }
   }
+#undef SRCNN_L3_PREFETCH
+#undef SRCNN_L3_T_PREFETCH
 
+#ifdef SRCNN_L3_TIMING
+  if (threadIdx.x == 0)
+    for (int k = 0; k < 4; k++) g_l3_timing[blockIdx.x][k] = tacc[k];
+#endif
   // ---- block reduction of the partial gradients, waves in order ----
   __syncthreads();
   for (int w = 0; w < nwaves; w++) {
@@ -251,11 +301,14 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
 }
 
 template <int N2, int F3>
-static size_t l3_lds_bytes(int npx2, int w3, int h3) {
-  const int w3p = w3 + 2 * (F3 - 1), h3p = h3 + 2 * (F3 - 1);
-  const size_t a2 = ((size_t)(npx2 + 8) * (N2 + 4) + 3) & ~size_t(3);
-  const size_t w3s = ((size_t)F3 * F3 * N2 + 3) & ~size_t(3);
-  const size_t d3 = ((size_t)w3p * h3p + 3) & ~size_t(3);
+static size_t l3_lds_bytes(int npx2, int w2) {
+  const size_t nch = (npx2 + 31) / 32;
+  const size_t a2 = nch * 32 * N2;
+  const size_t q = ((size_t)npx2 * F3 * F3 + 3) & ~size_t(3);
   const size_t red = (size_t)((N2 + 31) / 32) * 1024;
-  return (a2 + w3s + d3 + red) * sizeof(float);
+  const size_t d3 = nch * 32 + (size_t)(F3 - 1) * (w2 + 1) + 4;
+  return (a2 + (q > red ? q : red) + d3) * sizeof(float);
 }
+
+// L3 outputs per thread the kernel's T prefetch covers
+constexpr int kL3MaxOut = 2 * kL3Threads;

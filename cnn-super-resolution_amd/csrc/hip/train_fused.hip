@@ -2,7 +2,7 @@
 // middle layer (f2 == 1), e.g. the reference default n1=64, n2=32, f1=9, f3=5.
 //
 // The reference runs one OpenCL kernel per op (ConfigBasedDataPipeline.cpp:
-// 359-482): 3 forward, last delta, 2 deltas, 3 gradient kernels, every tensor
+// 200-323): 3 forward, last delta, 2 deltas, 3 gradient kernels, every tensor
 // round-tripping through global memory and the gradients summed serially per
 // weight (backpropagate.cl:89-106).  Here the same mathematics runs as three
 // kernels plus a deterministic reduction:
@@ -10,7 +10,7 @@
 //   l12_fwd      L1 (f1 x f1 x 1 -> n1) and L2 (1x1, n1 -> n2) as fp32 MFMA
 //                implicit GEMMs per 32-pixel chunk; A1 goes to HBM (needed by
 //                backward) and through a per-wave LDS transpose into L2.
-//   l3_delta     per sample: A2 tile in LDS; L3 (f3 x f3 x n2 -> 1, VALU),
+//   l3_delta     per sample: A2 tile in LDS; L3 (f3 x f3 x n2 -> 1, MFMA Q trick),
 //                last-layer delta with the reference quirk, delta2 (MFMA over
 //                the 25 taps), gW3 (MFMA over pixels), gB3, squared error.
 //   d1_grad12    delta1 = relu'(A1) * (delta2 . W2^T) (MFMA), then gW2 and gW1
@@ -23,8 +23,6 @@
 // layer-by-layer dataflow.  Results are deterministic: the
 // sample -> block -> wave assignment is static and every sum has a fixed
 // order; no float atomics anywhere.
-#include <cstdlib>
-
 #include "common.hpp"
 #include "mfma.hpp"
 #include "ops.hpp"
@@ -481,8 +479,8 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   const int npx2 = ow * oh;
   const int pf = l3_prefetch_regs<N2, F3>(npx2);
   if (pf > 16) return 0;
-  const size_t lds3 = l3_lds_bytes<N2, F3>(npx2, w3, h3);
-  if (lds3 > 160 * 1024) return 0;
+  const size_t lds3 = l3_lds_bytes<N2, F3>(npx2, ow);
+  if (lds3 > 160 * 1024 || w3 * h3 > kL3MaxOut) return 0;
   const int g12 = grid_for_batch(batch, 1024);
   const int g3 = grid_for_batch(batch, 256);
   const int gd = grid_for_batch(batch, 512);
@@ -511,11 +509,7 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
                        B1, W2, B2, A1, A2, g);
     SRCNN_LAUNCH_TRY();
   }
-  static const int l3_ablate = [] {
-    const char* e = getenv("SRCNN_ABLATE_L3");  // diagnostics only
-    return e ? atoi(e) : 0;
-  }();
-  L3Geom lg{(int)w, (int)h, ow, oh, w3, h3, (int)batch, l3_ablate};
+  L3Geom lg{(int)w, (int)h, ow, oh, w3, h3, (int)batch};
   {
     SRCNN_PROFILE("l3_delta_fused", s);
     int rc = pf <= 10 ? launch_l3<N2, F3, 10>(A2, T, W3, B3, D2, slab3, sqs, lg, g3, lds3, s)
@@ -567,3 +561,12 @@ int train_fwd_bwd(const srcnn_net* net, const float* X, const float* T, uint32_t
 
 }  // namespace fused
 }  // namespace srcnn
+
+#ifdef SRCNN_L3_TIMING
+extern "C" __attribute__((visibility("default"))) int srcnn_debug_l3_timing(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(srcnn::fused::g_l3_timing), sizeof(srcnn::fused::g_l3_timing)) ==
+                 hipSuccess
+             ? 0
+             : -1;
+}
+#endif

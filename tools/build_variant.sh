@@ -1,0 +1,16 @@
+#!/bin/bash
+# Build a diagnostic variant of libsrcnn_hip.so with extra compile flags:
+#   tools/build_variant.sh <name> [-DFLAG ...]  -> cnn-super-resolution_amd/lib/variants/libsrcnn_hip_<name>.so
+set -e
+R=$(cd "$(dirname "$0")/.." && pwd)
+P=$R/cnn-super-resolution_amd
+name=$1; shift
+O=$P/build/variant_$name
+mkdir -p $O $P/lib/variants
+for f in runtime.cpp abi.cpp ops_generic.hip ops_fast.hip train_fused.hip; do
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -fvisibility=hidden -munsafe-fp-atomics \
+    -Wno-unused-result -I$R/include -I$P/csrc/hip "$@" -x hip -c $P/csrc/hip/$f -o $O/$f.o &
+done
+wait
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $P/lib/variants/libsrcnn_hip_$name.so $O/*.o
+echo built $P/lib/variants/libsrcnn_hip_$name.so
