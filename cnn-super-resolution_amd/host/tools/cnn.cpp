@@ -1,0 +1,254 @@
+// cnn -- the command line of the reference (src/Main_cl.cpp) on the MI355X
+// pipeline:
+//
+//   cnn [-h] [train] [dry] [profile] -c CONFIG -i IN [-o OUT] [-e EPOCHS]
+//       [--seed N] [--device D] [--validation-percent P] [--mini-batches M]
+//
+// forward:  IN is an image (PNG / PNM), OUT the upscaled result image
+// train:    IN is a directory of <name>_large.<ext> / <name>_small.<ext> pairs
+//           (ground truth / degraded input, tools/make_samples.py makes
+//           them), OUT the parameters.json written at the end.
+// Differences from the reference, on purpose: paths are joined with '/'
+// (the reference hard-codes "\\", src/Main_cl.cpp:284-287), the epoch
+// shuffle is seeded (--seed; the reference uses unseeded rand()), JPEG is
+// not decoded (see host/src/Image.hpp).
+#include <dirent.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <iostream>
+#include <map>
+#include <random>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "Config.hpp"
+#include "ConfigBasedDataPipeline.hpp"
+#include "Context.hpp"
+#include "Image.hpp"
+
+using namespace cnn_sr;
+
+namespace {
+
+struct Args {
+  bool train = false, dry = false, profile = false, help = false;
+  std::string config, in, out;
+  size_t epochs = 0;
+  uint64_t seed = 0;
+  bool seeded = false;
+  int device = 0;
+  size_t validation_percent = 20;  // src/Main_cl.cpp:87
+  size_t mini_batches = 2;         // src/Main_cl.cpp:88
+};
+
+void usage() {
+  std::cout
+      << "usage: cnn [-h] [train] [dry] [profile] -c CONFIG -i IN [-o OUT] [-e EPOCHS]\n"
+         "           [--seed N] [--device D] [--validation-percent P] [--mini-batches M]\n\n"
+         "  -h, --help            print this help\n"
+         "  train                 train mode\n"
+         "  dry                   do not store the result\n"
+         "  profile               print kernel execution times\n"
+         "  -c, --config CONFIG   CNN configuration (config.json)\n"
+         "  -i, --in IN           image during forward, samples directory during training\n"
+         "  -o, --out OUT         output path (result image or new parameters file)\n"
+         "  -e, --epochs EPOCHS   number of epochs during training\n"
+         "  --seed N              seed of the random parameters and the epoch shuffles\n"
+         "  --device D            HIP device index (default 0)\n"
+         "  --validation-percent  share of samples used for validation (default 20)\n"
+         "  --mini-batches M      mini-batches per epoch (default 2)\n";
+}
+
+bool parse(int argc, char** argv, Args& a) {
+  for (int i = 1; i < argc; ++i) {
+    std::string s = argv[i];
+    auto value = [&](const char* name) -> std::string {
+      if (i + 1 >= argc) throw std::runtime_error(std::string("missing value for ") + name);
+      return argv[++i];
+    };
+    if (s == "-h" || s == "--help" || s == "help") a.help = true;
+    else if (s == "train") a.train = true;
+    else if (s == "dry") a.dry = true;
+    else if (s == "profile") a.profile = true;
+    else if (s == "-c" || s == "--config") a.config = value("--config");
+    else if (s == "-i" || s == "--in") a.in = value("--in");
+    else if (s == "-o" || s == "--out") a.out = value("--out");
+    else if (s == "-e" || s == "--epochs") a.epochs = std::stoul(value("--epochs"));
+    else if (s == "--seed") { a.seed = std::stoull(value("--seed")); a.seeded = true; }
+    else if (s == "--device") a.device = std::stoi(value("--device"));
+    else if (s == "--validation-percent") a.validation_percent = std::stoul(value("--validation-percent"));
+    else if (s == "--mini-batches") a.mini_batches = std::stoul(value("--mini-batches"));
+    else throw std::runtime_error("unknown argument '" + s + "'");
+  }
+  if (a.help) return false;
+  if (a.config.empty() || a.in.empty()) throw std::runtime_error("--config and --in are required");
+  return true;
+}
+
+/** <base>_large.* / <base>_small.* pairs of a samples directory
+ * (src/Main_cl.cpp:267-301), sorted by base name. */
+std::vector<std::pair<std::string, std::string>> training_samples(const std::string& dir) {
+  DIR* d = opendir(dir.c_str());
+  if (!d) throw srcnn::IOException("cannot open samples directory '" + dir + "'");
+  std::map<std::string, std::pair<std::string, std::string>> by_base;
+  while (dirent* e = readdir(d)) {
+    std::string f = e->d_name;
+    if (f == "." || f == "..") continue;
+    size_t dot = f.rfind('.');
+    std::string stem = dot == std::string::npos ? f : f.substr(0, dot);
+    auto ends = [&](const char* suf) {
+      size_t n = std::strlen(suf);
+      return stem.size() > n && stem.compare(stem.size() - n, n, suf) == 0;
+    };
+    if (ends("_large")) by_base[stem.substr(0, stem.size() - 6)].first = dir + "/" + f;
+    else if (ends("_small")) by_base[stem.substr(0, stem.size() - 6)].second = dir + "/" + f;
+    else std::cout << "'" << f << "' is not a <name>_large / <name>_small image. Skipping sample" << std::endl;
+  }
+  closedir(d);
+  std::vector<std::pair<std::string, std::string>> out;
+  for (auto& kv : by_base) {
+    if (kv.second.first.empty() || kv.second.second.empty())
+      std::cout << "Only 1 image for pair with name '" << kv.first << "'. Skipping sample" << std::endl;
+    else
+      out.push_back(kv.second);
+  }
+  return out;
+}
+
+/** load + luma (normalised) on the device (src/Main_cl.cpp:303-318) */
+void prepare_image(DataPipeline& p, const std::string& path, ImageData& img, MemoryHandle& data,
+                   MemoryHandle& luma) {
+  srcnn::image::load(path, img, 4);
+  p.extract_luma(img, data, luma, true);
+}
+
+int forward(ConfigBasedDataPipeline& p, const Args& a) {
+  auto& ctx = *p.context();
+  ImageData img;
+  SampleAllocationPool sample;
+  prepare_image(p, a.in, img, sample.input_data, sample.input_luma);
+  p.subtract_mean(sample.input_luma);
+  sample.input_w = img.w;
+  sample.input_h = img.h;
+  ctx.block();
+  GpuAllocationPool pools;
+  p.forward(pools.layer_1, pools.layer_2, pools.layer_3, sample);
+  if (!a.dry && !a.out.empty()) p.write_result_image(a.out.c_str(), img, sample);
+  ctx.block();
+  return 0;
+}
+
+int train(ConfigBasedDataPipeline& p, const Args& a) {
+  auto& ctx = *p.context();
+  auto files = training_samples(a.in);
+  if (files.empty()) throw std::runtime_error("no training samples in '" + a.in + "'");
+  const size_t nval = files.size() * a.validation_percent / 100, ntrain = files.size() - nval;
+  if (nval == 0) std::cout << "[WARNING] Validation set is empty" << std::endl;
+  else
+    std::cout << "validation_set_size: " << nval << "/" << files.size() << " = "
+              << (nval * 100.0f / files.size()) << "%" << std::endl;
+  srcnn::require(ntrain > 0, "Training set is empty");
+  p.set_mini_batch_size(ntrain / a.mini_batches + a.mini_batches);  // src/Main_cl.cpp:128-129
+
+  GpuAllocationPool pools;
+  for (auto& f : files) {
+    ImageData large, small;
+    SampleAllocationPool s;
+    prepare_image(p, f.first, large, s.expected_data, s.expected_luma);
+    prepare_image(p, f.second, small, s.input_data, s.input_luma);
+    srcnn::require(large.w == small.w && large.h == small.h,
+                   "sample pair sizes differ: " + f.first + " / " + f.second);
+    p.subtract_mean(s.input_luma);
+    s.input_w = small.w;
+    s.input_h = small.h;
+    ctx.block();
+    ctx.raw_memory(s.input_data)->release();  // 3-channel images are not needed any more
+    ctx.raw_memory(s.expected_data)->release();
+    pools.samples.push_back(s);
+  }
+  const size_t px = pools.samples[0].input_w * pools.samples[0].input_h;
+
+  std::mt19937_64 rng(a.seeded ? a.seed : std::random_device{}());
+  std::vector<size_t> order(pools.samples.size());
+  bool error = false;
+  for (size_t epoch = 0; epoch < a.epochs; ++epoch) {
+    // new random validation / training split every epoch (src/Main_cl.cpp:244-261)
+    for (size_t i = 0; i < order.size(); ++i) order[i] = i;
+    std::shuffle(order.begin(), order.end(), rng);
+    std::vector<SampleAllocationPool*> val, tr;
+    for (size_t i = 0; i < order.size(); ++i) (i < nval ? val : tr).push_back(&pools.samples[order[i]]);
+
+    p.execute_batch(true, pools, tr);
+    p.update_parameters(pools.layer_1, pools.layer_2, pools.layer_3, tr.size());
+
+    if (!val.empty() && (epoch % 25 == 0 || epoch == a.epochs - 1)) {
+      float err = p.execute_batch(false, pools, val);
+      if (std::isnan(err)) {
+        std::cout << "Error: squared error is NAN, after " << epoch << "/" << a.epochs << " epochs"
+                  << std::endl;
+        error = true;
+        break;
+      }
+      float mean = err / val.size();
+      std::cout << "[" << epoch << "] mean validation error: " << mean << " (" << (mean / px)
+                << " per px)" << std::endl;
+    }
+  }
+  if (!a.dry && !a.out.empty())
+    p.write_params_to_file(a.out.c_str(), pools.layer_1, pools.layer_2, pools.layer_3);
+  ctx.block();
+  std::cout << "DONE" << std::endl;
+  return error ? 1 : 0;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  Args a;
+  try {
+    if (!parse(argc, argv, a)) {
+      usage();
+      return 0;
+    }
+  } catch (const std::exception& e) {
+    std::cout << e.what() << std::endl;
+    usage();
+    return 1;
+  }
+  if (!a.dry && a.out.empty()) {
+    std::cout << "Either provide out path or do the dry run" << std::endl;
+    return 1;
+  }
+  if (a.profile)
+    std::cout << "!!! RUNNING IN PROFILING MODE !!!" << std::endl;
+  if (a.train)
+    std::cout << "Training mode, epochs: " << a.epochs << std::endl
+              << "Training samples directory: " << a.in << std::endl
+              << "Output: " << (a.dry ? "-" : a.out) << std::endl;
+  else
+    std::cout << "Forward mode" << std::endl
+              << "Input image: " << a.in << std::endl
+              << "Output: " << (a.dry ? "-" : a.out) << std::endl;
+  try {
+    ConfigReader reader;
+    Config cfg = reader.read(a.config.c_str());
+    std::cout << cfg << std::endl;
+    srcnn::Context context;
+    context.init(a.profile, a.device);
+    int rc;
+    {
+      ConfigBasedDataPipeline pipeline(cfg, &context);
+      if (a.seeded) pipeline.set_random_seed(a.seed);
+      pipeline.init(DataPipeline::LOAD_KERNEL_ALL);
+      rc = a.train ? train(pipeline, a) : forward(pipeline, a);
+    }
+    return rc;
+  } catch (const std::exception& e) {
+    std::cout << "[ERROR] " << e.what() << std::endl;
+    return 1;
+  }
+}
