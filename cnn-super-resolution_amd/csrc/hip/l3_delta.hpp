@@ -5,20 +5,24 @@
 //   squared error    squared_error.cl:60-69 (validation metric)
 //   delta2           layer_deltas.cl:79-123, MFMA over the f3*f3 taps
 //   gW3 / gB3        backpropagate.cl:89-112, MFMA over the A2 pixels
-// 8 waves per block, one block per CU; the next sample's A2 tile is
-// prefetched into registers while the current one is processed.
+// 8 waves per block, one block per CU, grid-strided over samples.
 //
 // L3 forward has one output channel, so it is not a GEMM as written.  It is
 // split into a GEMM and a gather ("Q trick"):
 //   Q[q][tap] = sum_c A2[q][c] * W3[tap][c]        (MFMA, M = pixels, N = taps, K = channels)
 //   A3[p]     = B3 + sum_tap Q[p + off(tap)][tap]  (25 LDS reads per output)
-// which moves the 5x5x32 window sums from LDS-bound VALU onto the matrix
-// cores.  Q lives in LDS next to the A2 tile (stride K3: conflict-free reads).
+// which moves the 5x5x32 window sums from LDS-bound VALU onto the matrix cores.
 //
-// A2 LDS image: rows of N2 floats, 16-byte quads XOR-swizzled by row
-// (quad q of row p at q ^ ((p >> 1) & (N2/4 - 1))), so both the per-pixel
-// column reads of the MFMA A operand and the per-channel row reads are
-// (at most 2-way) bank-conflict free without padding.
+// LDS holds two tile-sized regions used ping-pong: region `cur` holds this
+// sample's A2, the other first holds Q and, once the L3 gather has consumed
+// Q, receives the NEXT sample's A2 by LDS-DMA (global_load_lds, no
+// registers) while delta2 / gW3 run.  The next sample swaps the roles.
+//
+// A2 LDS image: rows of N2 floats, 16-byte quads XOR-swizzled by row (quad
+// q of row p at q ^ ((p >> 1) & (N2/4 - 1))): the per-pixel column reads of
+// the MFMA A operand and the per-channel row reads are at most 2-way bank
+// conflicted without padding.  The DMA realises the swizzle by choosing each
+// lane's global source quad.
 #ifdef SRCNN_L3_TIMING
 // diagnostics build only: per-block cycles spent between the phase barriers
 __device__ unsigned long long g_l3_timing[1024][4];
@@ -44,11 +48,8 @@ struct L3Geom {
 };
 
 constexpr int kL3Threads = 512;
-
-template <int N2, int F3>
-__host__ __device__ constexpr int l3_prefetch_regs(int npx2) {
-  return (npx2 * (N2 / 4) + kL3Threads - 1) / kL3Threads;
-}
+constexpr int kL3TPF = 2;  // L3 outputs per thread (w3 * h3 <= kL3TPF * 512)
+constexpr int kL3MaxOut = kL3TPF * kL3Threads;
 
 // float index of A2[p][n] in the swizzled LDS image
 template <int N2>
@@ -57,7 +58,25 @@ __device__ __forceinline__ int a2_at(int p, int n) {
   return p * N2 + 4 * ((n >> 2) ^ ((p >> 1) & (NQ - 1))) + (n & 3);
 }
 
-template <int N2, int F3, int PF>
+// LDS geometry shared by host and device (floats)
+template <int N2, int F3>
+struct L3Lds {
+  int region;  // one ping-pong region: max(A2 tile, Q, reduction scratch)
+  int d3off;   // delta3 grid offset (F3-1) * (w2 + 1)
+  int nd3;     // delta3 grid size (zero tail covers chunk overrun)
+  __host__ __device__ L3Lds(int w2, int h2) {
+    const int npx2 = w2 * h2, nch = (npx2 + 31) / 32;
+    int r = npx2 * N2;
+    if (npx2 * F3 * F3 > r) r = npx2 * F3 * F3;
+    if (((N2 + 31) / 32) * 1024 > r) r = ((N2 + 31) / 32) * 1024;
+    region = (r + 3) & ~3;
+    d3off = (F3 - 1) * (w2 + 1);
+    nd3 = nch * 32 + d3off + 4;
+  }
+  __host__ __device__ size_t bytes() const { return (2 * (size_t)region + nd3) * sizeof(float); }
+};
+
+template <int N2, int F3>
 __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
     const float* __restrict__ A2, const float* __restrict__ T, const float* __restrict__ W3,
     const float* __restrict__ B3, float* __restrict__ D2, float* __restrict__ slab3,
@@ -71,25 +90,24 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int npx2 = g.w2 * g.h2;
   const int nch = (npx2 + 31) / 32;
+  const L3Lds<N2, F3> L(g.w2, g.h2);
   // delta3 on the A2 grid: delta3(y, x) at d3g[(y + F3-1) * w2 + x + F3-1], zero
   // elsewhere (w3 = w2 - (F3-1), so a row's F3-1 leading columns are the zero
   // border of the previous row's wrap).  delta3(y - dy, x - dx) for A2 pixel
   // p = y*w2 + x is then d3g[p + (F3-1)*(w2+1) - (dy*w2 + dx)]: one add.
-  const int d3off = (F3 - 1) * (g.w2 + 1);
-  const int nd3 = nch * 32 + d3off + 4;
-  float* a2s = smem;                          // [nch*32][N2] swizzled (rows >= npx2 zero)
-  float* qs = a2s + nch * 32 * N2;            // [npx2][K3]
-  float* d3g = qs + ((npx2 * K3 + 3) & ~3);   // [nd3]
-  float* red = qs;                            // end-of-kernel reduction scratch (aliases qs)
+  const int d3off = L.d3off;
+  float* d3g = smem + 2 * L.region;
+  float* red = smem;  // end-of-kernel reduction scratch
 
   const int tid = threadIdx.x;
   const int lane = mfma::lane_id(), wave = mfma::wave_id();
   const int h = lane >> 5, li = lane & 31;
   constexpr int nwaves = kL3Threads / 64;
   const int pad = (g.W - g.w3) / 2;  // last_layer_delta.cl:25
+  const int nq = npx2 * NQ;          // 16-byte quads per A2 tile
+  const int ndma = (nq + 63) / 64;   // DMA instructions per tile (64 quads each)
 
-  for (int i = tid; i < nd3; i += kL3Threads) d3g[i] = 0.0f;
-  for (int i = npx2 * N2 + tid; i < nch * 32 * N2; i += kL3Threads) a2s[i] = 0.0f;
+  for (int i = tid; i < L.nd3; i += kL3Threads) d3g[i] = 0.0f;
 
   // B operand of Q: W3[tap = li][c = 2s + h]
   float wq[KC];
@@ -114,65 +132,71 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
   for (int u = 0; u < NT2; u++) gacc[u] = zero16();
   float gb3 = 0.0f, sq = 0.0f;
 
-  // register prefetch of one A2 tile: PF float4 per thread
-  float4 pf[PF];
-  const int nq = npx2 * NQ;
-#define SRCNN_L3_PREFETCH(SAMPLE)                                                        \
+  // A2 tile of SAMPLE -> region DST by LDS-DMA: instruction k writes image
+  // quads [64k, 64k + 64); lane j fetches the global quad that the swizzle
+  // places at image quad 64k + j.
+#define SRCNN_L3_A2_DMA(SAMPLE, DST)                                                     \
   do {                                                                                   \
-    const float4* src_ = reinterpret_cast<const float4*>(A2 + (size_t)(SAMPLE)*npx2 * N2); \
-    int t_ = tid; /* opaque: addresses are formed at the load, never held (spilled) */   \
-    asm volatile("" : "+v"(t_));                                                         \
-    _Pragma("unroll") for (int k = 0; k < PF; k++) {                                     \
-      const int i_ = t_ + k * kL3Threads;                                                \
-      pf[k] = i_ < nq ? src_[i_] : make_float4(0.f, 0.f, 0.f, 0.f);                      \
+    const float* src_ = A2 + (size_t)(SAMPLE)*npx2 * N2;                                 \
+    int l_ = lane; /* opaque: addresses are formed at the load, never held */            \
+    asm volatile("" : "+v"(l_));                                                         \
+    for (int k_ = wave; k_ < ndma; k_ += nwaves) {                                       \
+      const int f_ = 64 * k_ + l_;                                                       \
+      if (f_ < nq) {                                                                     \
+        const int p_ = f_ / NQ, j_ = f_ - p_ * NQ;                                       \
+        const int q_ = j_ ^ ((p_ >> 1) & (NQ - 1));                                      \
+        __builtin_amdgcn_global_load_lds(                                                \
+            (const void*)(src_ + p_ * N2 + 4 * q_),                                      \
+            (__attribute__((address_space(3))) void*)((DST) + 256 * k_), 16, 0, 0);      \
+      }                                                                                  \
     }                                                                                    \
   } while (0)
-  if ((int)blockIdx.x < g.batch) SRCNN_L3_PREFETCH(blockIdx.x);
 
-#ifdef SRCNN_L3_TIMING
-  unsigned long long tacc[4] = {0, 0, 0, 0}, tlast = clock64();
-#endif
-  const int nout = g.w3 * g.h3;
   // ground truth of this thread's L3 outputs, prefetched one sample ahead
-  constexpr int TPF = 2;  // outputs per thread (w3 * h3 <= TPF * 512)
-  float tpf[TPF];
+  const int nout = g.w3 * g.h3;
+  float tpf[kL3TPF];
 #define SRCNN_L3_T_PREFETCH(SAMPLE)                                                    \
   do {                                                                                 \
-    _Pragma("unroll") for (int k = 0; k < TPF; k++) {                                  \
+    _Pragma("unroll") for (int k = 0; k < kL3TPF; k++) {                               \
       const int t_ = tid + k * kL3Threads;                                             \
       const int y_ = t_ / g.w3, x_ = t_ - (t_ / g.w3) * g.w3;                          \
       tpf[k] = t_ < nout ? T[(size_t)(SAMPLE)*g.W * g.H + (size_t)(y_ + pad) * g.W + x_ + pad] : 0.f; \
     }                                                                                  \
   } while (0)
-  if ((int)blockIdx.x < g.batch) SRCNN_L3_T_PREFETCH(blockIdx.x);
+
+  int cur = 0;
+  if ((int)blockIdx.x < g.batch) {
+    SRCNN_L3_A2_DMA(blockIdx.x, smem);
+    SRCNN_L3_T_PREFETCH(blockIdx.x);
+  }
+#ifdef SRCNN_L3_TIMING
+  unsigned long long tacc[4] = {0, 0, 0, 0}, tlast = clock64();
+#endif
 
   for (int sample = blockIdx.x; sample < g.batch; sample += gridDim.x) {
-    __syncthreads();  // previous sample fully consumed a2s / d3p
-    SRCNN_L3_TICK(0);
-#pragma unroll
-    for (int k = 0; k < PF; k++) {
-      const int i = tid + k * kL3Threads;
-      if (i < nq) {
-        const int p = i / NQ, q = i - p * NQ;
-        *reinterpret_cast<float4*>(a2s + a2_at<N2>(p, 4 * q)) = pf[k];
-      }
-    }
-    float tcur[TPF];
-#pragma unroll
-    for (int k = 0; k < TPF; k++) tcur[k] = tpf[k];
-    if (sample + (int)gridDim.x < g.batch) {
-      SRCNN_L3_PREFETCH(sample + gridDim.x);
-      SRCNN_L3_T_PREFETCH(sample + gridDim.x);
-    }
+    // this sample's A2 DMA has landed in every wave; the previous sample's
+    // readers of both regions and of d3g are done
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    SRCNN_L3_TICK(1);
+    SRCNN_L3_TICK(0);
+    const float* a2s = smem + cur * L.region;
+    float* other = smem + (cur ^ 1) * L.region;
+    float* qs = other;  // [npx2][K3]
+    float tcur[kL3TPF];
+#pragma unroll
+    for (int k = 0; k < kL3TPF; k++) tcur[k] = tpf[k];
+    const bool has_next = sample + (int)gridDim.x < g.batch;
+    if (has_next) SRCNN_L3_T_PREFETCH(sample + gridDim.x);
 
-    // ---- Q = A2 . W3^T per 32-pixel chunk ----
+    // ---- Q = A2 . W3^T per 32-pixel chunk (rows past npx2 are discarded) ----
     for (int c = wave; c < nch; c += nwaves) {
       const int p = c * 32 + li;
       f32x16 acc = zero16();
+      float av[KC];
 #pragma unroll
-      for (int s = 0; s < KC; s++) acc = mma(a2s[a2_at<N2>(p, 2 * s + h)], wq[s], acc);
+      for (int s = 0; s < KC; s++) av[s] = a2s[a2_at<N2>(p, 2 * s + h)];
+#pragma unroll
+      for (int s = 0; s < KC; s++) acc = mma(av[s], wq[s], acc);
       if (li < K3) {
 #pragma unroll
         for (int r = 0; r < 16; r++) {
@@ -182,11 +206,11 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
       }
     }
     __syncthreads();
-    SRCNN_L3_TICK(2);
+    SRCNN_L3_TICK(1);
 
     // ---- L3 = B3 + diagonal sums of Q; last delta; squared error ----
 #pragma unroll
-    for (int k = 0; k < TPF; k++) {
+    for (int k = 0; k < kL3TPF; k++) {
       const int t = tid + k * kL3Threads;
       if (t < nout) {
         const int y = t / g.w3, x = t - y * g.w3;
@@ -205,36 +229,28 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
       }
     }
     __syncthreads();
-    SRCNN_L3_TICK(3);
+    SRCNN_L3_TICK(2);
 
-    // ---- per 32-pixel chunk: delta2 (MFMA over taps) and gW3 (MFMA over pixels) ----
+    // Q is consumed: the next sample's A2 streams into its region meanwhile
+    if (has_next) SRCNN_L3_A2_DMA(sample + gridDim.x, other);
+
+    // ---- delta2[q][n] = [A2 > 0] * sum_tap delta3(q - off(tap)) W3[tap][n] ----
     for (int c = wave; c < nch; c += nwaves) {
       const int c0 = c * 32;
-      // delta2[q][n] = [A2 > 0] * sum_tap delta3(q - off(tap)) W3[tap][n], q = c0 + li
       f32x16 acc[NT2];
 #pragma unroll
       for (int u = 0; u < NT2; u++) acc[u] = zero16();
+      float av[KS3];  // all A operands first: one LDS latency per chunk, not per MFMA
 #pragma unroll
       for (int s = 0; s < KS3; s++) {
         const int tap = 2 * s + h;
         const int o = tap < K3 ? (tap / F3) * g.w2 + tap % F3 : 0;
-        const float a = tap < K3 ? d3g[c0 + li + d3off - o] : 0.0f;
-#pragma unroll
-        for (int u = 0; u < NT2; u++) acc[u] = mma(a, wd[s][u], acc[u]);
+        av[s] = tap < K3 ? d3g[c0 + li + d3off - o] : 0.0f;
       }
-      // gW3[tap][n] += sum_p delta3(p - off(tap)) A2[p][n], p = c0 + 2s + h
-      // (rows >= npx2 of a2s and the d3g tail are zero: no bounds checks)
 #pragma unroll
-      for (int s = 0; s < 16; s++) {
-        const int p = c0 + 2 * s + h;
-        const float a = my_tap ? d3g[p + my_off] : 0.0f;
+      for (int s = 0; s < KS3; s++)
 #pragma unroll
-        for (int u = 0; u < NT2; u++) {
-          const int n = 32 * u + li;
-          gacc[u] = mma(a, n < N2 ? a2s[a2_at<N2>(p, n)] : 0.0f, gacc[u]);
-        }
-        if ((s & 7) == 7) __builtin_amdgcn_sched_barrier(0);  // bound the operand hoisting
-      }
+        for (int u = 0; u < NT2; u++) acc[u] = mma(av[s], wd[s][u], acc[u]);
 #pragma unroll
       for (int r = 0; r < 16; r++) {
         const int pr = c0 + crow(r, h);
@@ -250,8 +266,32 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
         }
       }
     }
+
+    // ---- gW3[tap][n] += sum_p delta3(p - off(tap)) A2[p][n] ----
+    // (the d3g tail is zero for p >= npx2; the A2 row is clamped in range)
+    for (int c = wave; c < nch; c += nwaves) {
+      const int c0 = c * 32;
+      float av[16], bv[16][NT2];  // operands first, then the MFMA chain
+#pragma unroll
+      for (int s = 0; s < 16; s++) {
+        const int p = c0 + 2 * s + h;
+        const int pb = min(p, npx2 - 1);
+        av[s] = my_tap ? d3g[p + my_off] : 0.0f;
+#pragma unroll
+        for (int u = 0; u < NT2; u++) {
+          const int n = 32 * u + li;
+          bv[s][u] = n < N2 ? a2s[a2_at<N2>(pb, n)] : 0.0f;
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < 16; s++)
+#pragma unroll
+        for (int u = 0; u < NT2; u++) gacc[u] = mma(av[s], bv[s][u], gacc[u]);
+    }
+    SRCNN_L3_TICK(3);
+    cur ^= 1;
   }
-#undef SRCNN_L3_PREFETCH
+#undef SRCNN_L3_A2_DMA
 #undef SRCNN_L3_T_PREFETCH
 
 #ifdef SRCNN_L3_TIMING
@@ -301,14 +341,6 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
 }
 
 template <int N2, int F3>
-static size_t l3_lds_bytes(int npx2, int w2) {
-  const size_t nch = (npx2 + 31) / 32;
-  const size_t a2 = nch * 32 * N2;
-  const size_t q = ((size_t)npx2 * F3 * F3 + 3) & ~size_t(3);
-  const size_t red = (size_t)((N2 + 31) / 32) * 1024;
-  const size_t d3 = nch * 32 + (size_t)(F3 - 1) * (w2 + 1) + 4;
-  return (a2 + (q > red ? q : red) + d3) * sizeof(float);
+static size_t l3_lds_bytes(int w2, int h2) {
+  return L3Lds<N2, F3>(w2, h2).bytes();
 }
-
-// L3 outputs per thread the kernel's T prefetch covers
-constexpr int kL3MaxOut = 2 * kL3Threads;

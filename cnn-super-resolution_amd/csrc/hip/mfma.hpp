@@ -34,7 +34,9 @@ __device__ __forceinline__ f32x16 zero16() {
 }
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
-__device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
+// wave index, provably uniform (SGPR): keeps per-wave LDS bases and DMA M0
+// values scalar instead of per-lane VGPRs
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 
 }  // namespace mfma
 }  // namespace srcnn

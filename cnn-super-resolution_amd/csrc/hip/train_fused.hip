@@ -40,15 +40,13 @@ constexpr int kXsMax = 1536;  // input sample / region tile (floats) staged in L
 struct Geom {
   int W, H;      // input sample
   int ow, oh;    // L1 (and L2) output
-  int rw, rh;    // region of L1 output handled per work item
-  int nrx, nry;  // regions per sample
   int batch;
 };
 
 // ---------------------------------------------------------------------------
-// Kernel 1: L1 (+ L2) forward
+// Kernel 1: L1 (+ L2) forward, one sample per work item
 // ---------------------------------------------------------------------------
-template <int N1, int N2, int F1, bool STORE_A1, bool DO_L2>
+template <int N1, int N2, int F1>
 __global__ __launch_bounds__(256, 2) void l12_fwd_kernel(
     const float* __restrict__ X, const float* __restrict__ W1, const float* __restrict__ B1,
     const float* __restrict__ W2, const float* __restrict__ B2, float* __restrict__ A1,
@@ -57,12 +55,12 @@ __global__ __launch_bounds__(256, 2) void l12_fwd_kernel(
   constexpr int NT2 = (N2 + 31) / 32, KS2 = N1 / 2;
   constexpr int TS = N1 + 1;  // padded row of the per-wave A1 transpose
   __shared__ float xs[kXsMax];
-  __shared__ float ts[DO_L2 ? 4 : 1][32][DO_L2 ? TS : 1];
-  __shared__ int gidx[4][32];
+  __shared__ float ts[4][32][TS];
 
   const int lane = mfma::lane_id(), wave = mfma::wave_id();
   const int h = lane >> 5, li = lane & 31;
-  const int tw = g.rw + F1 - 1;  // LDS row stride of the input tile
+  const int npx = g.ow * g.oh;
+  const int nch = (npx + 31) / 32;
 
   // B operands of L1: W1[tap = 2s + h][n = 32t + li]
   float w1f[KS1][NT1];
@@ -77,97 +75,78 @@ __global__ __launch_bounds__(256, 2) void l12_fwd_kernel(
 #pragma unroll
   for (int t = 0; t < NT1; t++) b1v[t] = B1[32 * t + li];
   // B operands of L2: W2[c = 2s + h][n = 32u + li]
-  float w2f[DO_L2 ? KS2 : 1][NT2];
+  float w2f[KS2][NT2];
   float b2v[NT2];
-  if constexpr (DO_L2) {
 #pragma unroll
-    for (int s = 0; s < KS2; s++)
+  for (int s = 0; s < KS2; s++)
 #pragma unroll
-      for (int u = 0; u < NT2; u++) {
-        const int n = 32 * u + li;
-        w2f[s][u] = n < N2 ? W2[(2 * s + h) * N2 + n] : 0.0f;
-      }
-#pragma unroll
-    for (int u = 0; u < NT2; u++) b2v[u] = (32 * u + li) < N2 ? B2[32 * u + li] : 0.0f;
-  }
-
-  const int per_sample = g.nry * g.nrx;
-  const int n_items = g.batch * per_sample;
-  for (int wi = blockIdx.x; wi < n_items; wi += gridDim.x) {
-    const int sample = wi / per_sample;
-    const int rr = wi - sample * per_sample;
-    const int ry = rr / g.nrx, rx = rr - ry * g.nrx;
-    const int oy0 = ry * g.rh, ox0 = rx * g.rw;
-    const int crh = min(g.rh, g.oh - oy0), crw = min(g.rw, g.ow - ox0);
-    const int th = crh + F1 - 1, tww = crw + F1 - 1;
-
-    __syncthreads();  // previous work item's readers are done with xs
-    const float* xsrc = X + (size_t)sample * g.W * g.H + (size_t)oy0 * g.W + ox0;
-    for (int i = threadIdx.x; i < th * tww; i += blockDim.x) {
-      const int iy = i / tww, ix = i - iy * tww;
-      xs[iy * tw + ix] = xsrc[(size_t)iy * g.W + ix];
+    for (int u = 0; u < NT2; u++) {
+      const int n = 32 * u + li;
+      w2f[s][u] = n < N2 ? W2[(2 * s + h) * N2 + n] : 0.0f;
     }
+#pragma unroll
+  for (int u = 0; u < NT2; u++) b2v[u] = (32 * u + li) < N2 ? B2[32 * u + li] : 0.0f;
+
+  for (int sample = blockIdx.x; sample < g.batch; sample += gridDim.x) {
+    __syncthreads();  // previous sample's readers are done with xs
+    const float* xsrc = X + (size_t)sample * g.W * g.H;
+    for (int i = threadIdx.x; i < g.W * g.H; i += blockDim.x) xs[i] = xsrc[i];
     __syncthreads();
 
-    const int npx = crh * crw;
-    const int nch = (npx + 31) / 32;
     for (int c = wave; c < nch; c += 4) {
       // this lane's own pixel (A-operand row li)
-      const int p = c * 32 + li;
-      const bool valid = p < npx;
-      const int pc = valid ? p : npx - 1;
-      const int iy = pc / crw, ix = pc - iy * crw;
-      const int xb = iy * tw + ix;
-      if (h == 0)
-        gidx[wave][li] = valid ? (sample * g.oh + oy0 + iy) * g.ow + ox0 + ix : -1;
+      const int pc = min(c * 32 + li, npx - 1);
+      const int iy = pc / g.ow, ix = pc - iy * g.ow;
+      const int xb = iy * g.W + ix;
 
       f32x16 acc1[NT1];
 #pragma unroll
       for (int t = 0; t < NT1; t++) acc1[t] = zero16();
 #pragma unroll
       for (int s = 0; s < KS1; s++) {
-        constexpr int dummy = 0;
-        (void)dummy;
         const int k0 = 2 * s, k1 = 2 * s + 1;
-        const int o0 = (k0 / F1) * tw + (k0 % F1);
-        const int o1 = k1 < K1 ? (k1 / F1) * tw + (k1 % F1) : 0;
+        const int o0 = (k0 / F1) * g.W + (k0 % F1);
+        const int o1 = k1 < K1 ? (k1 / F1) * g.W + (k1 % F1) : 0;
         const float a = xs[xb + (h ? o1 : o0)];
 #pragma unroll
         for (int t = 0; t < NT1; t++) acc1[t] = mma(a, w1f[s][t], acc1[t]);
       }
 
-      // epilogue L1: bias + ReLU (layer_uber_kernel.cl:88-95), store A1 (HWC)
+      // epilogue L1: bias + ReLU (layer_uber_kernel.cl:88-95), store A1 (HWC).
+      // Output row crow(r, h) of the chunk is pixel c*32 + crow(r, h) of the
+      // sample: the store address is a per-lane base plus an immediate.
+      const int q0 = c * 32 + 4 * h;  // pixel of register 0 of this lane half
+      float* a1row = A1 + ((size_t)sample * npx + q0) * N1 + li;
 #pragma unroll
       for (int r = 0; r < 16; r++) {
-        const int gp = gidx[wave][crow(r, h)];
+        const int rr = (r & 3) + 8 * (r >> 2);  // crow(r, h) - 4h
+        const bool ok = q0 + rr < npx;
 #pragma unroll
         for (int t = 0; t < NT1; t++) {
           const float v = fmaxf(acc1[t][r] + b1v[t], 0.0f);
-          if constexpr (STORE_A1) {
-            if (gp >= 0) A1[(size_t)gp * N1 + 32 * t + li] = v;
-          }
-          if constexpr (DO_L2) ts[wave][crow(r, h)][32 * t + li] = v;
+          if (ok) a1row[rr * N1 + 32 * t] = v;
+          ts[wave][crow(r, h)][32 * t + li] = v;
         }
       }
-      if constexpr (DO_L2) {
-        __builtin_amdgcn_wave_barrier();
-        f32x16 acc2[NT2];
+      __builtin_amdgcn_wave_barrier();
+      f32x16 acc2[NT2];
 #pragma unroll
-        for (int u = 0; u < NT2; u++) acc2[u] = zero16();
+      for (int u = 0; u < NT2; u++) acc2[u] = zero16();
 #pragma unroll
-        for (int s = 0; s < KS2; s++) {
-          const float a = ts[wave][li][2 * s + h];  // A1[pixel li][channel 2s+h]
+      for (int s = 0; s < KS2; s++) {
+        const float a = ts[wave][li][2 * s + h];  // A1[pixel li][channel 2s+h]
 #pragma unroll
-          for (int u = 0; u < NT2; u++) acc2[u] = mma(a, w2f[s][u], acc2[u]);
-        }
+        for (int u = 0; u < NT2; u++) acc2[u] = mma(a, w2f[s][u], acc2[u]);
+      }
+      float* a2row = A2 + ((size_t)sample * npx + q0) * N2 + li;
 #pragma unroll
-        for (int r = 0; r < 16; r++) {
-          const int gp = gidx[wave][crow(r, h)];
+      for (int r = 0; r < 16; r++) {
+        const int rr = (r & 3) + 8 * (r >> 2);
+        const bool ok = q0 + rr < npx;
 #pragma unroll
-          for (int u = 0; u < NT2; u++) {
-            const int n = 32 * u + li;
-            if (gp >= 0 && n < N2) A2[(size_t)gp * N2 + n] = fmaxf(acc2[u][r] + b2v[u], 0.0f);
-          }
+        for (int u = 0; u < NT2; u++) {
+          const int n = 32 * u + li;
+          if (ok && n < N2) a2row[rr * N2 + 32 * u] = fmaxf(acc2[u][r] + b2v[u], 0.0f);
         }
       }
       __builtin_amdgcn_wave_barrier();
@@ -177,6 +156,21 @@ __global__ __launch_bounds__(256, 2) void l12_fwd_kernel(
 
 
 #include "l3_delta.hpp"
+
+#ifdef SRCNN_D1_TIMING
+// diagnostics build only: wave 0's cycles per section of the chunk loop
+__device__ unsigned long long g_d1_timing[1024][6];
+#define SRCNN_D1_TICK(PH)                           \
+  do {                                              \
+    const unsigned long long now_ = clock64();      \
+    tacc[(PH + 5) % 6] += now_ - tlast;             \
+    tlast = now_;                                   \
+  } while (0)
+#else
+#define SRCNN_D1_TICK(PH) \
+  do {                    \
+  } while (0)
+#endif
 
 // ---------------------------------------------------------------------------
 // Kernel 3: delta1 + gW2/gB2 + gW1/gB1
@@ -195,13 +189,15 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
   constexpr int RED = (MT * NT1 + NT1 * NT2) * 16 * 64;
   static_assert(N2 % 2 == 0, "n2 must be even");
   constexpr int A1S = 4 * 32 * N1;        // per-wave A1 chunk staging (LDS-DMA target)
-  constexpr int LDS_MAIN = A1S + kXsMax + N1 * WS + 4 * 32 * DS;
+  constexpr int D2S = 32 * DS;            // per-wave delta2 chunk image [32][DS]
+  constexpr int D2K = (D2S + 63) / 64;    // 4-byte DMA instructions per chunk
+  constexpr int LDS_MAIN = A1S + 2 * kXsMax + N1 * WS + 4 * D2S;
   constexpr int LDS_TOTAL = LDS_MAIN > RED ? LDS_MAIN : RED;
   __shared__ __attribute__((aligned(16))) float smem[LDS_TOTAL];
   __shared__ int xbt[4][32];
   float* a1s = smem;                   // [4][32][N1], lane-linear DMA image of A1 rows
-  float* xs = smem + A1S;
-  float* w2s = xs + kXsMax;            // [N1][WS]: W2[c][n]
+  float* xsb = smem + A1S;             // [2][kXsMax]: X tile, double-buffered over samples
+  float* w2s = xsb + 2 * kXsMax;       // [N1][WS]: W2[c][n]
   float* d2w = w2s + N1 * WS;          // [4][32][DS]
 
   const int lane = mfma::lane_id(), wave = mfma::wave_id();
@@ -236,7 +232,7 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
 #pragma unroll
   for (int u = 0; u < NT2; u++) gb2[u] = 0.0f;
 
-  float* d2me = d2w + wave * 32 * DS;
+  float* d2me = d2w + wave * D2S;
   // A1 rows of one chunk -> this wave's LDS image by LDS-DMA (no registers):
   // instruction k moves floats [256k, 256k + 256) of the [32][N1] chunk; rows
   // past the sample re-read its last row (finite, and their delta2 rows are 0)
@@ -254,18 +250,66 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
           (const void*)src_, (__attribute__((address_space(3))) void*)(a1me + k * 256), 16, 0, 0); \
     }                                                                             \
   } while (0)
+  // delta2 rows of one chunk -> this wave's padded [32][DS] image by 4-byte
+  // LDS-DMA: image float f = 64k + lane of instruction k is delta2[row f/DS]
+  // [col f%DS] (the pad column re-reads col 0); rows past the sample re-read
+  // its last row and are zeroed in LDS before use
+#define SRCNN_D1_D2_DMA(SMP, C)                                                   \
+  do {                                                                            \
+    int l_ = lane;                                                                \
+    asm volatile("" : "+v"(l_));                                                  \
+    const float* base_ = D2 + (size_t)(SMP) * npx * N2;                           \
+    _Pragma("unroll") for (int k = 0; k < D2K; k++) {                             \
+      const int f_ = 64 * k + l_;                                                 \
+      const int r_ = f_ / DS, col_ = f_ - (f_ / DS) * DS;                         \
+      const int row_ = min((C) * 32 + r_, npx - 1);                               \
+      if (k < D2K - 1 || f_ < D2S)                                                \
+        __builtin_amdgcn_global_load_lds(                                         \
+            (const void*)(base_ + row_ * N2 + (col_ < N2 ? col_ : 0)),            \
+            (__attribute__((address_space(3))) void*)(d2me + 64 * k), 4, 0, 0);   \
+    }                                                                             \
+  } while (0)
   const int nch = (npx + 31) / 32;
   // A1[p][c] of this lane's accumulator slots, read from the LDS image at use
 #define SRCNN_D1_A1(T, R) a1me[crow(R, h) * N1 + 32 * (T) + li]
 
-  for (int sample = blockIdx.x; sample < g.batch; sample += gridDim.x) {
-    __syncthreads();
-    if (wave < nch) SRCNN_D1_A1_DMA(sample, wave);
-    {
-      const float* src = X + (size_t)sample * g.W * g.H;
-      for (int i = threadIdx.x; i < g.W * g.H; i += 256) xs[i] = src[i];
+#ifdef SRCNN_D1_TIMING
+  unsigned long long tacc[6] = {0, 0, 0, 0, 0, 0}, tlast = clock64();
+#endif
+  // X tile of a sample -> xs buffer by 4-byte LDS-DMA (lane-linear)
+  const int xn = g.W * g.H, xk = (xn + 63) / 64;
+#define SRCNN_D1_X_DMA(SMP, DST)                                                  \
+  do {                                                                            \
+    int l_ = lane;                                                                \
+    asm volatile("" : "+v"(l_));                                                  \
+    const float* src_ = X + (size_t)(SMP) * xn;                                   \
+    for (int k_ = wave; k_ < xk; k_ += 4)                                         \
+      if (64 * k_ + l_ < xn)                                                      \
+        __builtin_amdgcn_global_load_lds(                                         \
+            (const void*)(src_ + 64 * k_ + l_),                                   \
+            (__attribute__((address_space(3))) void*)((DST) + 64 * k_), 4, 0, 0); \
+  } while (0)
+
+  // software pipeline across samples: a wave's next (sample, chunk) operands
+  // are always in flight while it computes the current one; the next
+  // sample's X tile streams into the other buffer meanwhile
+  if ((int)blockIdx.x < g.batch) {
+    SRCNN_D1_X_DMA(blockIdx.x, xsb);
+    if (wave < nch) {
+      SRCNN_D1_A1_DMA(blockIdx.x, wave);
+      SRCNN_D1_D2_DMA(blockIdx.x, wave);
     }
+  }
+  int xbuf = 0;
+  for (int sample = blockIdx.x; sample < g.batch; sample += gridDim.x, xbuf ^= 1) {
+    // this sample's X tile (every wave's share) has landed; the previous
+    // sample's readers of the other X buffer are done
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    const float* xs = xsb + xbuf * kXsMax;
+    const int next = sample + (int)gridDim.x;
+    const bool has_next = next < g.batch;
+    if (has_next && wave >= nch) SRCNN_D1_X_DMA(next, xsb + (xbuf ^ 1) * kXsMax);
 
     for (int c = wave; c < nch; c += 4) {
       {  // this lane's own pixel -> X base offset table
@@ -273,23 +317,19 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
         const int y = p / g.ow, x = p - y * g.ow;
         if (h == 0) xbt[wave][li] = y * g.W + x;
       }
-      // stage the delta2 chunk [32 px][N2] (zero rows past the sample)
-      const float* dsrc = D2 + ((size_t)sample * npx + c * 32) * N2;
-      for (int i = lane; i < 32 * N2 / 4; i += 64) {
-        const int row = i / (N2 / 4), q = i - row * (N2 / 4);
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (c * 32 + row < npx) v = reinterpret_cast<const float4*>(dsrc)[i];
-        float* d = d2me + row * DS + 4 * q;
-        d[0] = v.x;
-        d[1] = v.y;
-        d[2] = v.z;
-        d[3] = v.w;
-      }
       // the A1 DMA of this chunk has landed (the delta2 loads above already
       // waited for the older VM ops; keep the wait explicit for the DMA)
+      SRCNN_D1_TICK(0);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_wave_barrier();
+      if (c == wave && has_next) SRCNN_D1_X_DMA(next, xsb + (xbuf ^ 1) * kXsMax);
+      if (c * 32 + 32 > npx) {  // delta2 rows past the sample -> 0 (one contiguous range)
+        int l_ = lane;
+        asm volatile("" : "+v"(l_));
+        for (int i = (npx - c * 32) * DS + l_; i < D2S; i += 64) d2me[i] = 0.0f;
+      }
 
+      SRCNN_D1_TICK(1);
       // delta1[p][c] = [A1 > 0] * sum_n delta2[p][n] * W2[c][n]  (layer_deltas.cl, f=1)
       f32x16 d1[NT1];
 #pragma unroll
@@ -309,6 +349,7 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
 #pragma unroll
         for (int r = 0; r < 16; r++) d1[t][r] = SRCNN_D1_A1(t, r) > 0.0f ? d1[t][r] : 0.0f;
 
+      SRCNN_D1_TICK(2);
       // gW2[c][n] += sum_p A1[p][c] delta2[p][n]; gB2[n] += sum_p delta2[p][n]
 #pragma unroll
       for (int s = 0; s < 16; s++) {
@@ -323,11 +364,19 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
         }
       }
 
+      SRCNN_D1_TICK(3);
       // next chunk's A1 DMA overlaps the gW1 MFMAs (the image's reads retired)
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
-      if (c + 4 < nch) SRCNN_D1_A1_DMA(sample, c + 4);
+      if (c + 4 < nch) {
+        SRCNN_D1_A1_DMA(sample, c + 4);
+        SRCNN_D1_D2_DMA(sample, c + 4);
+      } else if (has_next) {  // this wave's first chunk of the next sample
+        SRCNN_D1_A1_DMA(next, wave);
+        SRCNN_D1_D2_DMA(next, wave);
+      }
 
+      SRCNN_D1_TICK(4);
       // gW1[tap][c] += sum_p X[p + tap] delta1[p][c]; ones row -> gB1[c]
 #pragma unroll
       for (int s = 0; s < 16; s++) {
@@ -339,16 +388,20 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
 #pragma unroll
           for (int t = 0; t < NT1; t++) g1[m][t] = mma(a, d1[t][s], g1[m][t]);
         }
-#ifdef SRCNN_D1_SCHED
-        if ((s & (SRCNN_D1_SCHED - 1)) == SRCNN_D1_SCHED - 1) __builtin_amdgcn_sched_barrier(0);
-#endif
       }
+      SRCNN_D1_TICK(5);
       __builtin_amdgcn_wave_barrier();
     }
   }
 #undef SRCNN_D1_A1_DMA
+#undef SRCNN_D1_D2_DMA
+#undef SRCNN_D1_X_DMA
 #undef SRCNN_D1_A1
 
+#ifdef SRCNN_D1_TIMING
+  if (lane == 0 && wave == 0)
+    for (int k = 0; k < 6; k++) g_d1_timing[blockIdx.x][k] = tacc[k];
+#endif
   // ---- block reduction (waves in order) into LDS, then one slab per block ----
   __syncthreads();
   float* red = smem;
@@ -449,19 +502,19 @@ struct Net {
 
 static int grid_for_batch(uint32_t batch, int cap) { return (int)std::min<uint32_t>(batch, cap); }
 
-template <int N2, int F3, int PF>
+template <int N2, int F3>
 static int launch_l3(const float* A2, const float* T, const float* W3, const float* B3, float* D2,
                      float* slab3, float* sqs, const L3Geom& lg, int grid, size_t lds, hipStream_t s) {
-  static bool attr = false;  // the A2 tile exceeds the 64 KiB default dynamic LDS
+  static bool attr = false;  // two A2 tiles exceed the 64 KiB default dynamic LDS
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)l3_delta_kernel<N2, F3, PF>,
+    hipError_t e = hipFuncSetAttribute((const void*)l3_delta_kernel<N2, F3>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess)
       return fail(SRCNN_ERR_HIP, "hipFuncSetAttribute(l3_delta): %s", hipGetErrorString(e));
     attr = true;
   }
-  hipLaunchKernelGGL((l3_delta_kernel<N2, F3, PF>), dim3(grid), dim3(kL3Threads), lds, s, A2, T,
-                     W3, B3, D2, slab3, sqs, lg);
+  hipLaunchKernelGGL((l3_delta_kernel<N2, F3>), dim3(grid), dim3(kL3Threads), lds, s, A2, T, W3,
+                     B3, D2, slab3, sqs, lg);
   SRCNN_LAUNCH_TRY();
   return SRCNN_OK;
 }
@@ -476,10 +529,7 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   const int ow = w - F1 + 1, oh = h - F1 + 1;
   const int w3 = ow - F3 + 1, h3 = oh - F3 + 1;
   if ((int)(w * h) > kXsMax || w3 <= 0 || h3 <= 0) return 0;
-  const int npx2 = ow * oh;
-  const int pf = l3_prefetch_regs<N2, F3>(npx2);
-  if (pf > 16) return 0;
-  const size_t lds3 = l3_lds_bytes<N2, F3>(npx2, ow);
+  const size_t lds3 = l3_lds_bytes<N2, F3>(ow, oh);
   if (lds3 > 160 * 1024 || w3 * h3 > kL3MaxOut) return 0;
   const int g12 = grid_for_batch(batch, 1024);
   const int g3 = grid_for_batch(batch, 256);
@@ -502,18 +552,17 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   const float* B2 = W2 + N1 * N2;
   const float* W3 = B2 + N2;
   const float* B3 = W3 + F3 * F3 * N2;
-  Geom g{(int)w, (int)h, ow, oh, ow, oh, 1, 1, (int)batch};
+  Geom g{(int)w, (int)h, ow, oh, (int)batch};
   {
     SRCNN_PROFILE("l12_fwd_mfma", s);
-    hipLaunchKernelGGL((l12_fwd_kernel<N1, N2, F1, true, true>), dim3(g12), dim3(256), 0, s, X, W1,
+    hipLaunchKernelGGL((l12_fwd_kernel<N1, N2, F1>), dim3(g12), dim3(256), 0, s, X, W1,
                        B1, W2, B2, A1, A2, g);
     SRCNN_LAUNCH_TRY();
   }
   L3Geom lg{(int)w, (int)h, ow, oh, w3, h3, (int)batch};
   {
     SRCNN_PROFILE("l3_delta_fused", s);
-    int rc = pf <= 10 ? launch_l3<N2, F3, 10>(A2, T, W3, B3, D2, slab3, sqs, lg, g3, lds3, s)
-                      : launch_l3<N2, F3, 16>(A2, T, W3, B3, D2, slab3, sqs, lg, g3, lds3, s);
+    int rc = launch_l3<N2, F3>(A2, T, W3, B3, D2, slab3, sqs, lg, g3, lds3, s);
     if (rc) return rc;
   }
   {
@@ -562,6 +611,14 @@ int train_fwd_bwd(const srcnn_net* net, const float* X, const float* T, uint32_t
 }  // namespace fused
 }  // namespace srcnn
 
+#ifdef SRCNN_D1_TIMING
+extern "C" __attribute__((visibility("default"))) int srcnn_debug_d1_timing(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(srcnn::fused::g_d1_timing), sizeof(srcnn::fused::g_d1_timing)) ==
+                 hipSuccess
+             ? 0
+             : -1;
+}
+#endif
 #ifdef SRCNN_L3_TIMING
 extern "C" __attribute__((visibility("default"))) int srcnn_debug_l3_timing(unsigned long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(srcnn::fused::g_l3_timing), sizeof(srcnn::fused::g_l3_timing)) ==

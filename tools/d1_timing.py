@@ -1,5 +1,5 @@
-"""Phase timing of the l3_delta kernel (diagnostics build, tools/build_variant.sh
-l3t -DSRCNN_L3_TIMING): one training step, then per-phase cycles averaged
+"""Section timing of the d1_grad12 kernel, wave 0 of each block (diagnostics
+build: tools/build_variant.sh d1t -DSRCNN_D1_TIMING): one training step, then per-phase cycles averaged
 over blocks."""
 import ctypes
 import os
@@ -8,7 +8,7 @@ import sys
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["SRCNN_HIP_LIB"] = os.path.join(ROOT, "cnn-super-resolution_amd/lib/variants/libsrcnn_hip_l3t.so")
+os.environ["SRCNN_HIP_LIB"] = os.path.join(ROOT, "cnn-super-resolution_amd/lib/variants/libsrcnn_hip_d1t.so")
 sys.path[:0] = [ROOT, os.path.join(ROOT, "cnn-super-resolution_amd"), os.path.join(ROOT, "tests")]
 import torch  # noqa: E402
 import srcnn_amd as S  # noqa: E402
@@ -27,11 +27,11 @@ ws = torch.empty(nb // 4 + 64, device=dev)
 for _ in range(3):
     S.train_fwd_bwd(net, Xd, Td, 33, 33, B, p, g, None, ws, nb)
 torch.cuda.synchronize()
-buf = (ctypes.c_ulonglong * (1024 * 4))()
-assert S.lib().srcnn_debug_l3_timing(buf) == 0
-t = np.array(buf, dtype=np.float64).reshape(1024, 4)[:256]
-names = ["Q mfma", "L3 gather+delta3", "delta2+gW3 (wave 0)", "top wait (DMA+barrier)"]
+buf = (ctypes.c_ulonglong * (1024 * 6))()
+assert S.lib().srcnn_debug_d1_timing(buf) == 0
+t = np.array(buf, dtype=np.float64).reshape(1024, 6)[:512]
+names = ["wait DMA (+xbt)", "delta1", "gW2", "issue DMA", "gW1", "other (sample top, X tile)"]
 tot = t.sum(axis=1).mean()
 for i, n in enumerate(names):
-    print("%-18s %10.0f cycles/block  %5.1f%%  (%.0f per sample)" % (n, t[:, i].mean(), 100 * t[:, i].mean() / tot, t[:, i].mean() / 16))
+    print("%-18s %10.0f cycles/block  %5.1f%%  (%.0f per chunk)" % (n, t[:, i].mean(), 100 * t[:, i].mean() / tot, t[:, i].mean() / 40))
 print("total %.0f cycles/block = %.1f us at 2.2 GHz" % (tot, tot / 2.2e3))
