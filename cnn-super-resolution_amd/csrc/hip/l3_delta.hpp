@@ -234,59 +234,82 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
     // Q is consumed: the next sample's A2 streams into its region meanwhile
     if (has_next) SRCNN_L3_A2_DMA(sample + gridDim.x, other);
 
-    // ---- delta2[q][n] = [A2 > 0] * sum_tap delta3(q - off(tap)) W3[tap][n] ----
-    for (int c = wave; c < nch; c += nwaves) {
-      const int c0 = c * 32;
-      f32x16 acc[NT2];
+    // ---- per 32-pixel chunk: delta2 and gW3 MFMAs; the delta2 epilogue
+    // (relu' mask + store) of the PREVIOUS chunk is issued behind the current
+    // chunk's MFMAs, so the matrix core never waits for it ----
+    //   delta2[q][n] = [A2 > 0] * sum_tap delta3(q - off(tap)) W3[tap][n]
+    //   gW3[tap][n] += sum_p delta3(p - off(tap)) A2[p][n]
+    // (the d3g tail is zero for p >= npx2; the A2 row is clamped in range)
+    {
+      f32x16 prev[NT2];
+      int pc0 = -1;  // first pixel of the chunk whose delta2 is pending
+      float* d2s = D2 + (size_t)sample * npx2 * N2;
+      // epilogue of a finished chunk: rows c0 + 4h + rr (rr = crow(r,h) - 4h)
+#define SRCNN_L3_D2_EPILOGUE(C0, ACC)                                                  \
+  do {                                                                                 \
+    const int q0_ = (C0) + 4 * h;                                                      \
+    float m_[16][NT2];                                                                 \
+    _Pragma("unroll") for (int r = 0; r < 16; r++)                                     \
+      _Pragma("unroll") for (int u = 0; u < NT2; u++) {                                \
+        const int rr_ = (r & 3) + 8 * (r >> 2);                                        \
+        const int pr_ = min(q0_ + rr_, npx2 - 1);                                      \
+        const int n_ = 32 * u + li;                                                    \
+        m_[r][u] = n_ < N2 ? a2s[a2_at<N2>(pr_, n_)] : 0.0f;                           \
+      }                                                                                \
+    float* dst_ = d2s + (size_t)q0_ * N2 + li;                                         \
+    if ((C0) + 32 <= npx2) {                                                           \
+      _Pragma("unroll") for (int r = 0; r < 16; r++)                                   \
+        _Pragma("unroll") for (int u = 0; u < NT2; u++)                                \
+          if (32 * u + li < N2)                                                        \
+            dst_[((r & 3) + 8 * (r >> 2)) * N2 + 32 * u] =                             \
+                m_[r][u] > 0.0f ? (ACC)[u][r] : 0.0f;                                  \
+    } else {                                                                           \
+      _Pragma("unroll") for (int r = 0; r < 16; r++)                                   \
+        _Pragma("unroll") for (int u = 0; u < NT2; u++) {                              \
+          const int rr_ = (r & 3) + 8 * (r >> 2);                                      \
+          if (q0_ + rr_ < npx2 && 32 * u + li < N2)                                    \
+            dst_[rr_ * N2 + 32 * u] = m_[r][u] > 0.0f ? (ACC)[u][r] : 0.0f;            \
+        }                                                                              \
+    }                                                                                  \
+  } while (0)
+      for (int c = wave; c < nch; c += nwaves) {
+        const int c0 = c * 32;
+        float ad[KS3], ag[16], bg[16][NT2];
 #pragma unroll
-      for (int u = 0; u < NT2; u++) acc[u] = zero16();
-      float av[KS3];  // all A operands first: one LDS latency per chunk, not per MFMA
+        for (int s = 0; s < KS3; s++) {
+          const int tap = 2 * s + h;
+          const int o = tap < K3 ? (tap / F3) * g.w2 + tap % F3 : 0;
+          ad[s] = tap < K3 ? d3g[c0 + li + d3off - o] : 0.0f;
+        }
 #pragma unroll
-      for (int s = 0; s < KS3; s++) {
-        const int tap = 2 * s + h;
-        const int o = tap < K3 ? (tap / F3) * g.w2 + tap % F3 : 0;
-        av[s] = tap < K3 ? d3g[c0 + li + d3off - o] : 0.0f;
-      }
-#pragma unroll
-      for (int s = 0; s < KS3; s++)
-#pragma unroll
-        for (int u = 0; u < NT2; u++) acc[u] = mma(av[s], wd[s][u], acc[u]);
-#pragma unroll
-      for (int r = 0; r < 16; r++) {
-        const int pr = c0 + crow(r, h);
-        if (pr < npx2) {
+        for (int s = 0; s < 16; s++) {
+          const int p = c0 + 2 * s + h;
+          const int pb = min(p, npx2 - 1);
+          ag[s] = my_tap ? d3g[p + my_off] : 0.0f;
 #pragma unroll
           for (int u = 0; u < NT2; u++) {
             const int n = 32 * u + li;
-            if (n < N2) {
-              const float m = a2s[a2_at<N2>(pr, n)] > 0.0f ? 1.0f : 0.0f;
-              D2[((size_t)sample * npx2 + pr) * N2 + n] = acc[u][r] * m;
-            }
+            bg[s][u] = n < N2 ? a2s[a2_at<N2>(pb, n)] : 0.0f;
           }
         }
+        f32x16 acc[NT2];
+#pragma unroll
+        for (int u = 0; u < NT2; u++) acc[u] = zero16();
+#pragma unroll
+        for (int s = 0; s < KS3; s++)
+#pragma unroll
+          for (int u = 0; u < NT2; u++) acc[u] = mma(ad[s], wd[s][u], acc[u]);
+#pragma unroll
+        for (int s = 0; s < 16; s++)
+#pragma unroll
+          for (int u = 0; u < NT2; u++) gacc[u] = mma(ag[s], bg[s][u], gacc[u]);
+        if (pc0 >= 0) SRCNN_L3_D2_EPILOGUE(pc0, prev);
+#pragma unroll
+        for (int u = 0; u < NT2; u++) prev[u] = acc[u];
+        pc0 = c0;
       }
-    }
-
-    // ---- gW3[tap][n] += sum_p delta3(p - off(tap)) A2[p][n] ----
-    // (the d3g tail is zero for p >= npx2; the A2 row is clamped in range)
-    for (int c = wave; c < nch; c += nwaves) {
-      const int c0 = c * 32;
-      float av[16], bv[16][NT2];  // operands first, then the MFMA chain
-#pragma unroll
-      for (int s = 0; s < 16; s++) {
-        const int p = c0 + 2 * s + h;
-        const int pb = min(p, npx2 - 1);
-        av[s] = my_tap ? d3g[p + my_off] : 0.0f;
-#pragma unroll
-        for (int u = 0; u < NT2; u++) {
-          const int n = 32 * u + li;
-          bv[s][u] = n < N2 ? a2s[a2_at<N2>(pb, n)] : 0.0f;
-        }
-      }
-#pragma unroll
-      for (int s = 0; s < 16; s++)
-#pragma unroll
-        for (int u = 0; u < NT2; u++) gacc[u] = mma(av[s], bv[s][u], gacc[u]);
+      if (pc0 >= 0) SRCNN_L3_D2_EPILOGUE(pc0, prev);
+#undef SRCNN_L3_D2_EPILOGUE
     }
     SRCNN_L3_TICK(3);
     cur ^= 1;

@@ -344,11 +344,6 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
           d1[t] = mma(a, b, d1[t]);
         }
       }
-#pragma unroll
-      for (int t = 0; t < NT1; t++)
-#pragma unroll
-        for (int r = 0; r < 16; r++) d1[t][r] = SRCNN_D1_A1(t, r) > 0.0f ? d1[t][r] : 0.0f;
-
       SRCNN_D1_TICK(2);
       // gW2[c][n] += sum_p A1[p][c] delta2[p][n]; gB2[n] += sum_p delta2[p][n]
 #pragma unroll
@@ -363,6 +358,13 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
           for (int t = 0; t < NT1; t++) g2[t][u] = mma(SRCNN_D1_A1(t, s), b, g2[t][u]);
         }
       }
+
+      // relu' mask of delta1 (after the independent gW2 MFMAs, so the delta1
+      // chain has drained without stalling the matrix core)
+#pragma unroll
+      for (int t = 0; t < NT1; t++)
+#pragma unroll
+        for (int r = 0; r < 16; r++) d1[t][r] = SRCNN_D1_A1(t, r) > 0.0f ? d1[t][r] : 0.0f;
 
       SRCNN_D1_TICK(3);
       // next chunk's A1 DMA overlaps the gW1 MFMAs (the image's reads retired)
