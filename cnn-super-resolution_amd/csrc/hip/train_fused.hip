@@ -112,31 +112,64 @@ __global__ __launch_bounds__(256, 2) void l12_fwd_kernel(
         for (int t = 0; t < NT1; t++) acc1[t] = mma(a, w1f[s][t], acc1[t]);
       }
 
-      // epilogue L1: bias + ReLU (layer_uber_kernel.cl:88-95), store A1 (HWC).
-      // Output row crow(r, h) of the chunk is pixel c*32 + crow(r, h) of the
-      // sample: the store address is a per-lane base plus an immediate.
-      const int q0 = c * 32 + 4 * h;  // pixel of register 0 of this lane half
-      float* a1row = A1 + ((size_t)sample * npx + q0) * N1 + li;
+      // epilogue L1: bias + ReLU (layer_uber_kernel.cl:88-95) in place, into
+      // the per-wave LDS transpose that feeds L2's A operand.  The A1 stores
+      // (HWC) are issued after the L2 MFMAs, so they stream out while the
+      // matrix core works.  Output row crow(r, h) of the chunk is pixel
+      // c*32 + crow(r, h): the store address is a per-lane base plus an immediate.
 #pragma unroll
-      for (int r = 0; r < 16; r++) {
-        const int rr = (r & 3) + 8 * (r >> 2);  // crow(r, h) - 4h
-        const bool ok = q0 + rr < npx;
+      for (int r = 0; r < 16; r++)
 #pragma unroll
         for (int t = 0; t < NT1; t++) {
-          const float v = fmaxf(acc1[t][r] + b1v[t], 0.0f);
-          if (ok) a1row[rr * N1 + 32 * t] = v;
-          ts[wave][crow(r, h)][32 * t + li] = v;
+          acc1[t][r] = fmaxf(acc1[t][r] + b1v[t], 0.0f);
+          ts[wave][crow(r, h)][32 * t + li] = acc1[t][r];
         }
-      }
       __builtin_amdgcn_wave_barrier();
       f32x16 acc2[NT2];
 #pragma unroll
       for (int u = 0; u < NT2; u++) acc2[u] = zero16();
+      const int q0 = c * 32 + 4 * h;  // pixel of register 0 of this lane half
+      float* a1row = A1 + ((size_t)sample * npx + q0) * N1 + li;
+      const bool full = c * 32 + 32 <= npx;  // wave-uniform
+      if (full) {
+        // one scheduling region: per k-step 1 LDS read, NT2 MFMAs and 2 of
+        // the 32*NT1/16 A1 stores, interleaved so the stores stream out
+        // under the MFMAs
 #pragma unroll
-      for (int s = 0; s < KS2; s++) {
-        const float a = ts[wave][li][2 * s + h];  // A1[pixel li][channel 2s+h]
+        for (int s = 0; s < KS2; s++) {
+          const float a = ts[wave][li][2 * s + h];
 #pragma unroll
-        for (int u = 0; u < NT2; u++) acc2[u] = mma(a, w2f[s][u], acc2[u]);
+          for (int u = 0; u < NT2; u++) acc2[u] = mma(a, w2f[s][u], acc2[u]);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; r++)
+#pragma unroll
+          for (int t = 0; t < NT1; t++) {
+#ifndef SRCNN_L12_NO_A1STORE  // diagnostics only
+            a1row[((r & 3) + 8 * (r >> 2)) * N1 + 32 * t] = acc1[t][r];
+#endif
+          }
+        constexpr int kStoresPerStep = (16 * NT1 + KS2 - 1) / KS2;
+#pragma unroll
+        for (int s = 0; s < KS2; s++) {
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);              // DS read
+          __builtin_amdgcn_sched_group_barrier(0x008, NT2, 0);            // MFMA
+          __builtin_amdgcn_sched_group_barrier(0x040, kStoresPerStep, 0); // VMEM write
+        }
+      } else {
+#pragma unroll
+        for (int s = 0; s < KS2; s++) {
+          const float a = ts[wave][li][2 * s + h];
+#pragma unroll
+          for (int u = 0; u < NT2; u++) acc2[u] = mma(a, w2f[s][u], acc2[u]);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+          const int rr = (r & 3) + 8 * (r >> 2);  // crow(r, h) - 4h
+#pragma unroll
+          for (int t = 0; t < NT1; t++)
+            if (q0 + rr < npx) a1row[rr * N1 + 32 * t] = acc1[t][r];
+        }
       }
       float* a2row = A2 + ((size_t)sample * npx + q0) * N2 + li;
 #pragma unroll
@@ -191,10 +224,10 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
   constexpr int A1S = 4 * 32 * N1;        // per-wave A1 chunk staging (LDS-DMA target)
   constexpr int D2S = 32 * DS;            // per-wave delta2 chunk image [32][DS]
   constexpr int D2K = (D2S + 63) / 64;    // 4-byte DMA instructions per chunk
-  constexpr int LDS_MAIN = A1S + 2 * kXsMax + N1 * WS + 4 * D2S;
+  constexpr int D2P = 64 * D2K;           // per-wave staging stride (whole DMA instructions)
+  constexpr int LDS_MAIN = A1S + 2 * kXsMax + N1 * WS + 4 * D2P;
   constexpr int LDS_TOTAL = LDS_MAIN > RED ? LDS_MAIN : RED;
   __shared__ __attribute__((aligned(16))) float smem[LDS_TOTAL];
-  __shared__ int xbt[4][32];
   float* a1s = smem;                   // [4][32][N1], lane-linear DMA image of A1 rows
   float* xsb = smem + A1S;             // [2][kXsMax]: X tile, double-buffered over samples
   float* w2s = xsb + 2 * kXsMax;       // [N1][WS]: W2[c][n]
@@ -203,6 +236,9 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
   const int lane = mfma::lane_id(), wave = mfma::wave_id();
   const int h = lane >> 5, li = lane & 31;
   const int npx = g.ow * g.oh;
+  // (q + 0.5) / ow in fp32 is at least 0.5/ow away from an integer for the
+  // pixel counts here, so the truncation is an exact q / ow
+  const float inv_ow = 1.0f / (float)g.ow;
 
   for (int i = threadIdx.x; i < N1 * N2; i += blockDim.x) {
     const int c = i / N2, n = i - c * N2;
@@ -232,42 +268,39 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
 #pragma unroll
   for (int u = 0; u < NT2; u++) gb2[u] = 0.0f;
 
-  float* d2me = d2w + wave * D2S;
-  // A1 rows of one chunk -> this wave's LDS image by LDS-DMA (no registers):
-  // instruction k moves floats [256k, 256k + 256) of the [32][N1] chunk; rows
-  // past the sample re-read its last row (finite, and their delta2 rows are 0)
+  float* d2me = d2w + wave * D2P;
+  // One LDS-DMA instruction K of a chunk's operands (no registers):
+  //   K < 8:  A1 rows -> this wave's lane-linear [32][N1] image (16 B / lane)
+  //   K >= 8: delta2 rows -> this wave's padded [32][DS] image (4 B / lane;
+  //           the pad column re-reads col 0, lanes past the image write into
+  //           the staging padding)
+  // Rows past the sample re-read its last row (A1: finite, and the delta2
+  // rows there are zeroed in LDS before use).
+  constexpr int kA1K = 32 * N1 / 256;
+  constexpr int kDmaK = kA1K + D2K;
   float* a1me = a1s + wave * 32 * N1;
-#define SRCNN_D1_A1_DMA(SMP, C)                                                   \
+#define SRCNN_D1_DMA_K(SMP, C, K)                                                 \
   do {                                                                            \
-    int lo_ = 4 * lane; /* opaque: keeps the addresses out of the loop preheader */ \
-    asm volatile("" : "+v"(lo_));                                                 \
-    const float* base_ = A1 + (size_t)(SMP) * npx * N1;                           \
-    _Pragma("unroll") for (int k = 0; k < 32 * N1 / 256; k++) {                   \
-      const int f_ = k * 256 + lo_;                                               \
-      const int row_ = min((C) * 32 + f_ / N1, npx - 1);                          \
-      const float* src_ = base_ + (row_ * N1 + (f_ % N1));                        \
-      __builtin_amdgcn_global_load_lds(                                           \
-          (const void*)src_, (__attribute__((address_space(3))) void*)(a1me + k * 256), 16, 0, 0); \
-    }                                                                             \
-  } while (0)
-  // delta2 rows of one chunk -> this wave's padded [32][DS] image by 4-byte
-  // LDS-DMA: image float f = 64k + lane of instruction k is delta2[row f/DS]
-  // [col f%DS] (the pad column re-reads col 0); rows past the sample re-read
-  // its last row and are zeroed in LDS before use
-#define SRCNN_D1_D2_DMA(SMP, C)                                                   \
-  do {                                                                            \
-    int l_ = lane;                                                                \
+    int l_ = lane; /* opaque: the address is formed here, never held */           \
     asm volatile("" : "+v"(l_));                                                  \
-    const float* base_ = D2 + (size_t)(SMP) * npx * N2;                           \
-    _Pragma("unroll") for (int k = 0; k < D2K; k++) {                             \
-      const int f_ = 64 * k + l_;                                                 \
+    if ((K) < kA1K) {                                                             \
+      const int f_ = (K) * 256 + 4 * l_;                                          \
+      const int row_ = min((C) * 32 + f_ / N1, npx - 1);                          \
+      __builtin_amdgcn_global_load_lds(                                           \
+          (const void*)(A1 + (size_t)(SMP) * npx * N1 + (row_ * N1 + (f_ % N1))), \
+          (__attribute__((address_space(3))) void*)(a1me + (K) * 256), 16, 0, 0); \
+    } else {                                                                      \
+      const int f_ = 64 * ((K) - kA1K) + l_;                                      \
       const int r_ = f_ / DS, col_ = f_ - (f_ / DS) * DS;                         \
       const int row_ = min((C) * 32 + r_, npx - 1);                               \
-      if (k < D2K - 1 || f_ < D2S)                                                \
-        __builtin_amdgcn_global_load_lds(                                         \
-            (const void*)(base_ + row_ * N2 + (col_ < N2 ? col_ : 0)),            \
-            (__attribute__((address_space(3))) void*)(d2me + 64 * k), 4, 0, 0);   \
+      __builtin_amdgcn_global_load_lds(                                           \
+          (const void*)(D2 + (size_t)(SMP) * npx * N2 + row_ * N2 + (col_ < N2 ? col_ : 0)), \
+          (__attribute__((address_space(3))) void*)(d2me + 64 * ((K) - kA1K)), 4, 0, 0); \
     }                                                                             \
+  } while (0)
+#define SRCNN_D1_DMA_ALL(SMP, C)                                                  \
+  do {                                                                            \
+    _Pragma("unroll") for (int k_ = 0; k_ < kDmaK; k_++) SRCNN_D1_DMA_K(SMP, C, k_); \
   } while (0)
   const int nch = (npx + 31) / 32;
   // A1[p][c] of this lane's accumulator slots, read from the LDS image at use
@@ -295,10 +328,7 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
   // sample's X tile streams into the other buffer meanwhile
   if ((int)blockIdx.x < g.batch) {
     SRCNN_D1_X_DMA(blockIdx.x, xsb);
-    if (wave < nch) {
-      SRCNN_D1_A1_DMA(blockIdx.x, wave);
-      SRCNN_D1_D2_DMA(blockIdx.x, wave);
-    }
+    if (wave < nch) SRCNN_D1_DMA_ALL(blockIdx.x, wave);
   }
   int xbuf = 0;
   for (int sample = blockIdx.x; sample < g.batch; sample += gridDim.x, xbuf ^= 1) {
@@ -312,11 +342,6 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
     if (has_next && wave >= nch) SRCNN_D1_X_DMA(next, xsb + (xbuf ^ 1) * kXsMax);
 
     for (int c = wave; c < nch; c += 4) {
-      {  // this lane's own pixel -> X base offset table
-        const int p = min(c * 32 + li, npx - 1);
-        const int y = p / g.ow, x = p - y * g.ow;
-        if (h == 0) xbt[wave][li] = y * g.W + x;
-      }
       // the A1 DMA of this chunk has landed (the delta2 loads above already
       // waited for the older VM ops; keep the wait explicit for the DMA)
       SRCNN_D1_TICK(0);
@@ -370,33 +395,68 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
       // next chunk's A1 DMA overlaps the gW1 MFMAs (the image's reads retired)
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
-      if (c + 4 < nch) {
-        SRCNN_D1_A1_DMA(sample, c + 4);
-        SRCNN_D1_D2_DMA(sample, c + 4);
-      } else if (has_next) {  // this wave's first chunk of the next sample
-        SRCNN_D1_A1_DMA(next, wave);
-        SRCNN_D1_D2_DMA(next, wave);
-      }
-
-      SRCNN_D1_TICK(4);
-      // gW1[tap][c] += sum_p X[p + tap] delta1[p][c]; ones row -> gB1[c]
+      // gW1[tap][c] += sum_p X[p + tap] delta1[p][c]; ones row -> gB1[c].
+      // Hand-pipelined: the X gathers of step s+1 are issued before the
+      // MFMAs of step s, and the operand DMA of this wave's next work item
+      // (the next chunk, or its first chunk of the next sample, or when
+      // neither exists a harmless re-read of this one) is spread over the
+      // steps so its address math issues while the matrix core is busy.
+      {
+        const bool more = c + 4 < nch;
+        const int dsmp = more ? sample : (has_next ? next : sample);
+        const int dch = more ? c + 4 : (has_next ? wave : c);
+        // X offset of pixel row crow(s, h) of this chunk (rows past the
+        // sample clamp to its last pixel: their delta1 is 0)
+#define SRCNN_D1_XB(S)                                                              \
+  ([&]() {                                                                          \
+    const int q_ = min(c * 32 + crow((S), h), npx - 1);                             \
+    const int y_ = (int)(((float)q_ + 0.5f) * inv_ow);                              \
+    return q_ + y_ * (g.W - g.ow);                                                  \
+  }())
+#define SRCNN_D1_GATHER(XB, M)                                                      \
+  ([&]() {                                                                          \
+    float a_ = xs[(XB) + toff[M]];                                                  \
+    if (32 * (M) + 31 >= K1) a_ = tsel_x[M] != 0.0f ? a_ : tsel_1[M];               \
+    return a_;                                                                      \
+  }())
+        float acur[MT];
+        {
+          const int xb = SRCNN_D1_XB(0);
 #pragma unroll
-      for (int s = 0; s < 16; s++) {
-        const int xb = xbt[wave][crow(s, h)];
-#pragma unroll
-        for (int m = 0; m < MT; m++) {
-          float a = xs[xb + toff[m]];
-          if (32 * m + 31 >= K1) a = tsel_x[m] != 0.0f ? a : tsel_1[m];  // zero rows / ones row
-#pragma unroll
-          for (int t = 0; t < NT1; t++) g1[m][t] = mma(a, d1[t][s], g1[m][t]);
+          for (int m = 0; m < MT; m++) acur[m] = SRCNN_D1_GATHER(xb, m);
         }
+#pragma unroll
+        for (int s = 0; s < 16; s++) {
+          float anxt[MT];
+          if (s + 1 < 16) {
+            const int xb = SRCNN_D1_XB(s + 1);
+#pragma unroll
+            for (int m = 0; m < MT; m++) anxt[m] = SRCNN_D1_GATHER(xb, m);
+          }
+#pragma unroll
+          for (int m = 0; m < MT; m++)
+#pragma unroll
+            for (int t = 0; t < NT1; t++) g1[m][t] = mma(acur[m], d1[t][s], g1[m][t]);
+          if (2 * s < kDmaK) SRCNN_D1_DMA_K(dsmp, dch, 2 * s);
+          if (2 * s + 1 < kDmaK) SRCNN_D1_DMA_K(dsmp, dch, 2 * s + 1);
+          if (s + 1 < 16) {
+#pragma unroll
+            for (int m = 0; m < MT; m++) acur[m] = anxt[m];
+          }
+        }
+        if (32 < kDmaK) {  // more DMA instructions than two per step
+#pragma unroll
+          for (int k = 32; k < kDmaK; k++) SRCNN_D1_DMA_K(dsmp, dch, k);
+        }
+#undef SRCNN_D1_XB
+#undef SRCNN_D1_GATHER
       }
       SRCNN_D1_TICK(5);
       __builtin_amdgcn_wave_barrier();
     }
   }
-#undef SRCNN_D1_A1_DMA
-#undef SRCNN_D1_D2_DMA
+#undef SRCNN_D1_DMA_K
+#undef SRCNN_D1_DMA_ALL
 #undef SRCNN_D1_X_DMA
 #undef SRCNN_D1_A1
 
