@@ -208,14 +208,21 @@ def main():
     ap.add_argument("--path", choices=["auto", "generic"], default="auto")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    # rehearsal of the N>1 path on a single-GPU box (NOT a measurement):
+    # every rank on one device, gradients all-reduced over gloo
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl")
+    ap.add_argument("--all-ranks-on-device", type=int, default=None)
     args = ap.parse_args()
 
     import srcnn_amd as S
     from srcnn_amd import parallel
 
     rank, world, local = parallel.env_world()
-    torch.cuda.set_device(local if world > 1 else 0)
-    parallel.init("nccl", torch.device("cuda", local))
+    dev_index = local if world > 1 else 0
+    if args.all_ranks_on_device is not None:
+        dev_index = args.all_ranks_on_device
+    torch.cuda.set_device(dev_index)
+    parallel.init(args.dist_backend, torch.device("cuda", dev_index))
     S.set_path(0 if args.path == "auto" else 1)
     dev = torch.device("cuda", torch.cuda.current_device())
     stream = torch.cuda.current_stream().cuda_stream
