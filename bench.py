@@ -199,6 +199,47 @@ def cpu_baseline(net, tiles_min=16, budget_s=12.0):
                       "restatement (oracle/srcnn_oracle.c), OpenMP over tiles" % (done, el)}
 
 
+def forward_4k(S, net_t, frames=5, warmup=2, w=3840, h=2160):
+    """BASELINE.json configs[4]: forward-only inference of one 3840x2160 luma
+    frame (fused path), reported as input Mpix/s.  Time with events on the
+    stream the kernels run on; per-kernel split from srcnn_profile_*."""
+    net = S.Net(*net_t)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    stream = torch.cuda.current_stream().cuda_stream
+    rng = np.random.default_rng(4)
+    x = torch.from_numpy((rng.random(w * h, dtype=np.float32) - 0.5)).to(dev)
+    prm = torch.from_numpy(init_params(net_t, S.net_param_count(net))).to(dev)
+    n1, n2, f1, f2, f3 = net_t
+    out = torch.empty((w - (f1 + f2 + f3 - 3)) * (h - (f1 + f2 + f3 - 3)), device=dev)
+    nbytes = S.forward_workspace_bytes(net, w, h, 1)
+    ws = torch.empty(nbytes // 4 + 64, device=dev)
+    for _ in range(warmup):
+        S.forward(net, x, w, h, 1, prm, out, ws, nbytes, stream)
+    torch.cuda.synchronize()
+    S.profile_reset()
+    S.profile_enable(True)
+    t0 = time.perf_counter()
+    for _ in range(frames):
+        S.forward(net, x, w, h, 1, prm, out, ws, nbytes, stream)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    S.profile_enable(False)
+    stats = S.profile_stats()
+    ms = el / frames * 1e3
+    # algorithmic work (SURVEY.md 8(d)): the three layers over the frame
+    w1, h1 = w - f1 + 1, h - f1 + 1
+    w2, h2 = w1 - f2 + 1, h1 - f2 + 1
+    w3, h3 = w2 - f3 + 1, h2 - f3 + 1
+    flops = 2.0 * (w1 * h1 * n1 * f1 * f1 + w2 * h2 * n2 * n1 * f2 * f2 + w3 * h3 * n2 * f3 * f3)
+    kernels = {k: {"launches_per_frame": c / frames, "ms_per_frame": round(t / frames, 4)}
+               for k, (c, t) in stats.items()}
+    return {"frame": "%dx%d" % (w, h), "frames": frames, "ms_per_frame": round(ms, 4),
+            "mpix_s": round(w * h / (ms * 1e-3) / 1e6, 1),
+            "tflops": round(flops / (ms * 1e-3) / 1e12, 2),
+            "roofline_frac": round(flops / (ms * 1e-3) / 1e12 / PEAK_FP32_TFLOPS, 4),
+            "algorithmic_gflop_per_frame": round(flops / 1e9, 2), "kernels": kernels}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -207,6 +248,7 @@ def main():
     ap.add_argument("--batch", type=int, default=4096, help="tiles per GPU per step")
     ap.add_argument("--path", choices=["auto", "generic"], default="auto")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-forward", action="store_true", help="skip the 4K inference line")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     # rehearsal of the N>1 path on a single-GPU box (NOT a measurement):
     # every rank on one device, gradients all-reduced over gloo
@@ -315,6 +357,8 @@ def main():
             "kernels": kernels,
             "cpu_baseline": None,
         }
+        if world == 1 and not args.no_forward:
+            out["forward"] = forward_4k(S, net_t)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(net_t, budget_s=args.cpu_budget)
         print(json.dumps(out), flush=True)

@@ -333,7 +333,13 @@ size_t srcnn_forward_workspace_bytes(const srcnn_net* net, uint32_t w, uint32_t 
                                      uint32_t batch) {
   NetDims d;
   if (net_dims(net, w, h, &d) || batch == 0) return 0;
-  return align_up(d.s1 * batch * sizeof(float)) + align_up(d.s2 * batch * sizeof(float));
+  size_t generic = align_up(d.s1 * batch * sizeof(float)) + align_up(d.s2 * batch * sizeof(float));
+  size_t fused = 0;
+  if (fast_enabled() &&
+      srcnn::fused::forward(net, nullptr, w, h, batch, nullptr, nullptr, nullptr, 0, nullptr, true,
+                            &fused) != 1)
+    fused = 0;
+  return std::max(generic, fused);
 }
 
 int srcnn_forward(const srcnn_net* net, const float* X, uint32_t w, uint32_t h, uint32_t batch,
@@ -346,6 +352,11 @@ int srcnn_forward(const srcnn_net* net, const float* X, uint32_t w, uint32_t h, 
   const size_t need = srcnn_forward_workspace_bytes(net, w, h, batch);
   if (ws_bytes < need)
     return fail(SRCNN_ERR_WORKSPACE, "forward: workspace %zu B < %zu B", ws_bytes, need);
+  if (fast_enabled()) {  // fused gfx950 inference (forward_fused.hip)
+    int rc = srcnn::fused::forward(net, X, w, h, batch, params, out, ws, ws_bytes,
+                                   as_stream(stream), false, nullptr);
+    if (rc != 0) return rc < 0 ? rc : SRCNN_OK;
+  }
   size_t off[6];
   srcnn_net_offsets(net, off);
   float* A1 = static_cast<float*>(ws);

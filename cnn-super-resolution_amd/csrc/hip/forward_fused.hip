@@ -1,0 +1,269 @@
+// forward_fused.hip -- gfx950 inference (forward only) for SRCNN nets with a
+// 1x1 middle layer (f2 == 1), for frames of any size (4K and up).
+//
+// The reference runs three layer launches with A1 and A2 round-tripping
+// through global memory (ConfigBasedDataPipeline.cpp:200-241, kernel
+// layer_uber_kernel.cl:36-96).  Here:
+//
+//   fwd_l12q  per 32 x RH region of L1/L2 outputs: L1 (f1 x f1 x 1 -> n1) and
+//             L2 (1x1, n1 -> n2) as fp32 MFMA implicit GEMMs, then the L3
+//             "Q trick" GEMM  Q[p][tap] = sum_c A2[p][c] * W3[tap][c]; only Q
+//             (f3*f3 floats per pixel) leaves the CU -- A1 and A2 never reach HBM.
+//   fwd_l3g   per 32 x 16 tile of outputs: A3[p] = B3 + sum_tap Q[p + off(tap)][tap]
+//             from an LDS copy of the Q rows the tile needs (no ReLU: SKIP_RELU).
+//
+// A region chunk is one region row of 32 pixels, so a chunk's outputs are
+// contiguous in the frame.  Rows / columns past the frame are computed on
+// clamped-in-range (or don't-care) inputs and never stored.
+#include "common.hpp"
+#include "mfma.hpp"
+#include "ops.hpp"
+
+namespace srcnn {
+namespace fused {
+
+using mfma::crow;
+using mfma::f32x16;
+using mfma::mma;
+using mfma::zero16;
+
+namespace {
+
+constexpr int kFwdRW = 32;        // region width (one chunk per region row)
+constexpr int kFwdXs = 1536;      // input tile floats staged in LDS
+constexpr int kGatherTW = 32;     // L3 gather tile: 32 x 16 outputs
+constexpr int kGatherTH = 16;
+
+struct FwdGeom {
+  int W, H;      // input frame
+  int ow, oh;    // L1 / L2 output
+  int rh;        // region rows
+  int nrx, nry;  // regions per frame
+  int batch;
+};
+
+template <int N1, int N2, int F1, int F3>
+__global__ __launch_bounds__(256, 2) void fwd_l12q_kernel(
+    const float* __restrict__ X, const float* __restrict__ W1, const float* __restrict__ B1,
+    const float* __restrict__ W2, const float* __restrict__ B2, const float* __restrict__ W3,
+    float* __restrict__ Q, FwdGeom g) {
+  constexpr int K1 = F1 * F1, KS1 = (K1 + 1) / 2, NT1 = N1 / 32;
+  constexpr int NT2 = (N2 + 31) / 32, KS2 = N1 / 2, KC = N2 / 2;
+  constexpr int K3 = F3 * F3;
+  constexpr int TW = kFwdRW + F1 - 1;  // LDS row stride of the input tile
+  constexpr int TS = N1 + 1;           // per-wave transpose row (A1, then A2)
+  static_assert(K3 <= 32 && N2 <= 32 && N2 % 2 == 0, "Q tile shape");
+  __shared__ float xs[kFwdXs];
+  __shared__ float ts[4][32][TS];
+  __shared__ float w3s[32][N2 + 1];  // W3[tap][c] (taps >= K3 zero), padded rows
+
+  const int lane = mfma::lane_id(), wave = mfma::wave_id();
+  const int h = lane >> 5, li = lane & 31;
+
+  // B operands: W1[tap = 2s+h][32t+li], W2[c = 2s+h][32u+li], W3[tap = li][c = 2s+h]
+  float w1f[KS1][NT1];
+#pragma unroll
+  for (int s = 0; s < KS1; s++)
+#pragma unroll
+    for (int t = 0; t < NT1; t++) {
+      const int tap = 2 * s + h;
+      w1f[s][t] = tap < K1 ? W1[tap * N1 + 32 * t + li] : 0.0f;
+    }
+  float b1v[NT1];
+#pragma unroll
+  for (int t = 0; t < NT1; t++) b1v[t] = B1[32 * t + li];
+  float w2f[KS2][NT2];
+#pragma unroll
+  for (int s = 0; s < KS2; s++)
+#pragma unroll
+    for (int u = 0; u < NT2; u++) {
+      const int n = 32 * u + li;
+      w2f[s][u] = n < N2 ? W2[(2 * s + h) * N2 + n] : 0.0f;
+    }
+  float b2v[NT2];
+#pragma unroll
+  for (int u = 0; u < NT2; u++) b2v[u] = (32 * u + li) < N2 ? B2[32 * u + li] : 0.0f;
+  for (int i = threadIdx.x; i < 32 * N2; i += 256) {
+    const int tap = i / N2, c = i - tap * N2;
+    w3s[tap][c] = tap < K3 ? W3[i] : 0.0f;
+  }
+
+  const int per_frame = g.nrx * g.nry;
+  const int n_items = g.batch * per_frame;
+  for (int wi = blockIdx.x; wi < n_items; wi += gridDim.x) {
+    const int n = wi / per_frame, rr = wi - n * per_frame;
+    const int ry = rr / g.nrx, rx = rr - ry * g.nrx;
+    const int oy0 = ry * g.rh, ox0 = rx * kFwdRW;
+    const int crh = min(g.rh, g.oh - oy0), crw = min(kFwdRW, g.ow - ox0);
+    const int th = crh + F1 - 1, tw = crw + F1 - 1;
+
+    __syncthreads();  // the previous region's readers are done with xs
+    const float* xsrc = X + (size_t)n * g.W * g.H + (size_t)oy0 * g.W + ox0;
+    for (int i = threadIdx.x; i < th * TW; i += 256) {
+      const int iy = i / TW, ix = i - iy * TW;
+      xs[i] = ix < tw ? xsrc[(size_t)iy * g.W + ix] : 0.0f;
+    }
+    __syncthreads();
+
+    for (int c = wave; c < crh; c += 4) {  // chunk = region row c, pixel li
+      const int xb = c * TW + li;
+      f32x16 acc1[NT1];
+#pragma unroll
+      for (int t = 0; t < NT1; t++) acc1[t] = zero16();
+#pragma unroll
+      for (int s = 0; s < KS1; s++) {
+        const int k0 = 2 * s, k1 = 2 * s + 1;
+        const int o0 = (k0 / F1) * TW + (k0 % F1);
+        const int o1 = k1 < K1 ? (k1 / F1) * TW + (k1 % F1) : 0;
+        const float a = xs[xb + (h ? o1 : o0)];
+#pragma unroll
+        for (int t = 0; t < NT1; t++) acc1[t] = mma(a, w1f[s][t], acc1[t]);
+      }
+      // L1 bias + ReLU -> transpose (A operand of L2)
+#pragma unroll
+      for (int r = 0; r < 16; r++)
+#pragma unroll
+        for (int t = 0; t < NT1; t++)
+          ts[wave][crow(r, h)][32 * t + li] = fmaxf(acc1[t][r] + b1v[t], 0.0f);
+      __builtin_amdgcn_wave_barrier();
+      f32x16 acc2[NT2];
+#pragma unroll
+      for (int u = 0; u < NT2; u++) acc2[u] = zero16();
+#pragma unroll
+      for (int s = 0; s < KS2; s++) {
+        const float a = ts[wave][li][2 * s + h];
+#pragma unroll
+        for (int u = 0; u < NT2; u++) acc2[u] = mma(a, w2f[s][u], acc2[u]);
+      }
+      // L2 bias + ReLU -> the same transpose (its L2 reads have retired)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int r = 0; r < 16; r++)
+#pragma unroll
+        for (int u = 0; u < NT2; u++) {
+          const int nn = 32 * u + li;
+          if (nn < N2) ts[wave][crow(r, h)][nn] = fmaxf(acc2[u][r] + b2v[u], 0.0f);
+        }
+      __builtin_amdgcn_wave_barrier();
+      // Q = A2 . W3^T for the chunk's 32 pixels
+      f32x16 accq = zero16();
+#pragma unroll
+      for (int s = 0; s < KC; s++) accq = mma(ts[wave][li][2 * s + h], w3s[li][2 * s + h], accq);
+      // Q[pixel][tap]: per register two 25-float runs (lane = tap)
+      float* qrow = Q + (((size_t)n * g.oh + oy0 + c) * g.ow + ox0) * K3;
+      if (li < K3) {
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+          const int px = crow(r, h);
+          if (px < crw) qrow[px * K3 + li] = accq[r];
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+}
+
+template <int F3>
+__global__ __launch_bounds__(256, 2) void fwd_l3g_kernel(const float* __restrict__ Q,
+                                                         const float* __restrict__ B3,
+                                                         float* __restrict__ out, int ow, int oh,
+                                                         int ntx, int nty, int batch) {
+  constexpr int K3 = F3 * F3;
+  constexpr int QW = kGatherTW + F3 - 1, QH = kGatherTH + F3 - 1;
+  __shared__ float qt[QH * QW * K3];
+  const int w3 = ow - F3 + 1, h3 = oh - F3 + 1;
+  const float b3 = B3[0];
+  const int per_frame = ntx * nty;
+  for (int wi = blockIdx.x; wi < batch * per_frame; wi += gridDim.x) {
+    const int n = wi / per_frame, rr = wi - n * per_frame;
+    const int ty0 = (rr / ntx) * kGatherTH, tx0 = (rr % ntx) * kGatherTW;
+    const int qh = min(QH, oh - ty0), qw = min(QW, ow - tx0);
+    __syncthreads();
+    for (int j = 0; j < qh; j++) {  // row j of Q: qw pixels x K3 floats, contiguous
+      const float* src = Q + (((size_t)n * oh + ty0 + j) * ow + tx0) * K3;
+      for (int i = threadIdx.x; i < qw * K3; i += 256) qt[j * QW * K3 + i] = src[i];
+    }
+    __syncthreads();
+    const int tx = threadIdx.x % kGatherTW;
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      const int ty = threadIdx.x / kGatherTW + 8 * k;
+      const int y = ty0 + ty, x = tx0 + tx;
+      if (y < h3 && x < w3) {
+        float acc = 0.0f;
+#pragma unroll
+        for (int dy = 0; dy < F3; dy++)
+#pragma unroll
+          for (int dx = 0; dx < F3; dx++)
+            acc += qt[((ty + dy) * QW + tx + dx) * K3 + dy * F3 + dx];
+        out[((size_t)n * h3 + y) * w3 + x] = acc + b3;
+      }
+    }
+  }
+}
+
+template <int N1, int N2, int F1, int F3>
+int run_forward(const float* X, uint32_t w, uint32_t h, uint32_t batch, const float* params,
+                float* out, void* ws, size_t ws_bytes, hipStream_t s, bool query_only,
+                size_t* need) {
+  constexpr int K3 = F3 * F3;
+  const int ow = (int)w - F1 + 1, oh = (int)h - F1 + 1;
+  if (ow < F3 || oh < F3) return 0;
+  // region rows: the input tile (32 + f1 - 1) x (rh + f1 - 1) fits the LDS tile,
+  // a multiple of the 4 waves
+  int rh = (kFwdXs / (kFwdRW + F1 - 1) - (F1 - 1)) / 4 * 4;
+  if (rh <= 0) return 0;
+  rh = std::min(rh, oh);
+  const size_t qbytes = (size_t)batch * ow * oh * K3 * sizeof(float);
+  if (query_only) {
+    *need = qbytes;
+    return 1;
+  }
+  if (ws_bytes < qbytes)
+    return fail(SRCNN_ERR_WORKSPACE, "fused forward: workspace %zu B < %zu B", ws_bytes, qbytes);
+  float* Q = static_cast<float*>(ws);
+  const float* W1 = params;
+  const float* B1 = W1 + F1 * F1 * N1;
+  const float* W2 = B1 + N1;
+  const float* B2 = W2 + N1 * N2;
+  const float* W3 = B2 + N2;
+  const float* B3 = W3 + F3 * F3 * N2;
+  FwdGeom g{(int)w, (int)h, ow, oh, rh, (ow + kFwdRW - 1) / kFwdRW, (oh + rh - 1) / rh, (int)batch};
+  const long items = (long)g.batch * g.nrx * g.nry;
+  {
+    SRCNN_PROFILE("fwd_l12q_mfma", s);
+    hipLaunchKernelGGL((fwd_l12q_kernel<N1, N2, F1, F3>), dim3((unsigned)std::min<long>(items, 2048)),
+                       dim3(256), 0, s, X, W1, B1, W2, B2, W3, Q, g);
+    SRCNN_LAUNCH_TRY();
+  }
+  {
+    SRCNN_PROFILE("fwd_l3_gather", s);
+    const int w3 = ow - F3 + 1, h3 = oh - F3 + 1;
+    const int ntx = (w3 + kGatherTW - 1) / kGatherTW, nty = (h3 + kGatherTH - 1) / kGatherTH;
+    const long tiles = (long)batch * ntx * nty;
+    hipLaunchKernelGGL((fwd_l3g_kernel<F3>), dim3((unsigned)std::min<long>(tiles, 4096)), dim3(256),
+                       0, s, Q, B3, out, ow, oh, ntx, nty, (int)batch);
+    SRCNN_LAUNCH_TRY();
+  }
+  return 1;
+}
+
+}  // namespace
+
+int forward(const srcnn_net* net, const float* X, uint32_t w, uint32_t h, uint32_t batch,
+            const float* params, float* out, void* ws, size_t ws_bytes, hipStream_t s,
+            bool query_only, size_t* need) {
+  if (net->f2 != 1) return 0;
+#define SRCNN_FWD_CASE(A, B, C, D)                                                       \
+  if (net->n1 == A && net->n2 == B && net->f1 == C && net->f3 == D)                     \
+    return run_forward<A, B, C, D>(X, w, h, batch, params, out, ws, ws_bytes, s, query_only, need);
+  SRCNN_FWD_CASE(64, 32, 9, 5)  // reference default
+  SRCNN_FWD_CASE(32, 16, 9, 5)  // example_config.json
+#undef SRCNN_FWD_CASE
+  return 0;
+}
+
+}  // namespace fused
+}  // namespace srcnn

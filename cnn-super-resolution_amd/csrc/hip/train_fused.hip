@@ -304,7 +304,11 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
   } while (0)
   const int nch = (npx + 31) / 32;
   // A1[p][c] of this lane's accumulator slots, read from the LDS image at use
+#ifndef SRCNN_D1_PURE_MFMA
 #define SRCNN_D1_A1(T, R) a1me[crow(R, h) * N1 + 32 * (T) + li]
+#else  // diagnostics only: no LDS operands (results invalid)
+#define SRCNN_D1_A1(T, R) __int_as_float(crow(R, h) * N1 + 32 * (T) + li + c)
+#endif
 
 #ifdef SRCNN_D1_TIMING
   unsigned long long tacc[6] = {0, 0, 0, 0, 0, 0}, tlast = clock64();
@@ -362,10 +366,18 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
 #pragma unroll
       for (int s = 0; s < KD; s++) {
         const int n = 2 * s + h;
+#ifndef SRCNN_D1_PURE_MFMA
         const float a = n < N2 ? d2me[li * DS + n] : 0.0f;
+#else
+        const float a = __int_as_float(li * DS + n + c);
+#endif
 #pragma unroll
         for (int t = 0; t < NT1; t++) {
+#ifndef SRCNN_D1_PURE_MFMA
           const float b = n < N2 ? w2s[(32 * t + li) * WS + n] : 0.0f;
+#else
+          const float b = __int_as_float((32 * t + li) * WS + n);
+#endif
           d1[t] = mma(a, b, d1[t]);
         }
       }
@@ -377,7 +389,11 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
 #pragma unroll
         for (int u = 0; u < NT2; u++) {
           const int n = 32 * u + li;
+#ifndef SRCNN_D1_PURE_MFMA
           const float b = n < N2 ? d2me[pr * DS + n] : 0.0f;
+#else
+          const float b = __int_as_float(pr * DS + n + c);
+#endif
           gb2[u] += b;
 #pragma unroll
           for (int t = 0; t < NT1; t++) g2[t][u] = mma(SRCNN_D1_A1(t, s), b, g2[t][u]);
@@ -407,6 +423,11 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
         const int dch = more ? c + 4 : (has_next ? wave : c);
         // X offset of pixel row crow(s, h) of this chunk (rows past the
         // sample clamp to its last pixel: their delta1 is 0)
+#ifndef SRCNN_D1_PURE_MFMA
+#define SRCNN_D1_XS(I) xs[I]
+#else
+#define SRCNN_D1_XS(I) __int_as_float(I)
+#endif
 #define SRCNN_D1_XB(S)                                                              \
   ([&]() {                                                                          \
     const int q_ = min(c * 32 + crow((S), h), npx - 1);                             \
@@ -415,7 +436,7 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
   }())
 #define SRCNN_D1_GATHER(XB, M)                                                      \
   ([&]() {                                                                          \
-    float a_ = xs[(XB) + toff[M]];                                                  \
+    float a_ = SRCNN_D1_XS((XB) + toff[M]);                                         \
     if (32 * (M) + 31 >= K1) a_ = tsel_x[M] != 0.0f ? a_ : tsel_1[M];               \
     return a_;                                                                      \
   }())
@@ -437,8 +458,10 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
           for (int m = 0; m < MT; m++)
 #pragma unroll
             for (int t = 0; t < NT1; t++) g1[m][t] = mma(acur[m], d1[t][s], g1[m][t]);
+#ifndef SRCNN_D1_PURE_MFMA
           if (2 * s < kDmaK) SRCNN_D1_DMA_K(dsmp, dch, 2 * s);
           if (2 * s + 1 < kDmaK) SRCNN_D1_DMA_K(dsmp, dch, 2 * s + 1);
+#endif
           if (s + 1 < 16) {
 #pragma unroll
             for (int m = 0; m < MT; m++) acur[m] = anxt[m];
@@ -449,6 +472,7 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
           for (int k = 32; k < kDmaK; k++) SRCNN_D1_DMA_K(dsmp, dch, k);
         }
 #undef SRCNN_D1_XB
+#undef SRCNN_D1_XS
 #undef SRCNN_D1_GATHER
       }
       SRCNN_D1_TICK(5);

@@ -361,6 +361,54 @@ def test_forward_vs_oracle(S, path):
     assert_close(H(out), ref, RTOL, "forward 256x256")
 
 
+FWD_FRAMES = [("default", 77, 45, 3), ("default", 300, 210, 1), ("example", 96, 64, 2),
+              ("default", 33, 33, 5), ("default", 41, 200, 1), ("wide", 64, 48, 1)]
+
+
+@pytest.mark.parametrize("name,w,h,b", FWD_FRAMES, ids=lambda v: str(v))
+def test_forward_frames_vs_oracle(S, path, name, w, h, b):
+    """srcnn_forward on ragged frames: partial 32-wide regions / 16-row
+    gather tiles at every edge, batches, both fused nets and a generic one."""
+    cfg = NETS[name]
+    net = S.Net(*cfg)
+    rng = np.random.default_rng(w * 1000 + h)
+    X, _ = make_batch(rng, b, w, h)
+    params = make_params(rng, cfg, sd=0.05)
+    ref = orc.forward(cfg, X, w, h, b, params)
+    nbytes = S.forward_workspace_bytes(net, w, h, b)
+    ws = torch.empty(nbytes // 4 + 64, dtype=torch.float32, device="cuda")
+    out = torch.full((ref.size,), float("nan"), dtype=torch.float32, device="cuda")
+    S.forward(net, D(X), w, h, b, D(params), out, ws, nbytes)
+    got = H(out)
+    assert np.isfinite(got).all()  # every output written
+    assert_close(got, ref, RTOL, "forward %s %dx%d b%d" % (name, w, h, b))
+
+
+def test_forward_large_frame_fused_vs_generic(S):
+    """A 1280x720 frame: the fused path against the generic layer-by-layer
+    path on the same device (the oracle would take minutes here)."""
+    cfg = NETS["default"]
+    net = S.Net(*cfg)
+    rng = np.random.default_rng(720)
+    w, h = 1280, 720
+    X, _ = make_batch(rng, 1, w, h)
+    params = make_params(rng, cfg, sd=0.05)
+    n_out = (w - 12) * (h - 12)
+    res = {}
+    for p in (0, 1):
+        S.set_path(p)
+        try:
+            nbytes = S.forward_workspace_bytes(net, w, h, 1)
+            ws = torch.empty(nbytes // 4 + 64, dtype=torch.float32, device="cuda")
+            out = torch.full((n_out,), float("nan"), dtype=torch.float32, device="cuda")
+            S.forward(net, D(X), w, h, 1, D(params), out, ws, nbytes)
+            res[p] = H(out)
+        finally:
+            S.set_path(0)
+    assert np.isfinite(res[0]).all()
+    assert_close(res[0], res[1], RTOL, "forward 1280x720 fused vs generic")
+
+
 # ----------------------------------------------------------------------------
 # full size (BASELINE config 2: default net, 33x33, batch 4096)
 # ----------------------------------------------------------------------------
