@@ -5,16 +5,21 @@
 // through global memory (ConfigBasedDataPipeline.cpp:200-241, kernel
 // layer_uber_kernel.cl:36-96).  Here:
 //
-//   fwd_l12q  per 32 x RH region of L1/L2 outputs: L1 (f1 x f1 x 1 -> n1) and
+//   fwd_l123  per 32 x RH region of L1/L2 outputs: L1 (f1 x f1 x 1 -> n1) and
 //             L2 (1x1, n1 -> n2) as fp32 MFMA implicit GEMMs, then the L3
-//             "Q trick" GEMM  Q[p][tap] = sum_c A2[p][c] * W3[tap][c]; only Q
-//             (f3*f3 floats per pixel) leaves the CU -- A1 and A2 never reach HBM.
-//   fwd_l3g   per 32 x 16 tile of outputs: A3[p] = B3 + sum_tap Q[p + off(tap)][tap]
-//             from an LDS copy of the Q rows the tile needs (no ReLU: SKIP_RELU).
+//             "Q trick" GEMM  Q[p][tap] = sum_c A2[p][c] * W3[tap][c], and the
+//             L3 window sums  sum_tap Q[p + off(tap)][tap]  of every output the
+//             region's A2 pixels reach, accumulated in LDS.  Only those partial
+//             output sums ((32 + f3 - 1) x (RH + f3 - 1) floats per region)
+//             leave the CU -- A1, A2 and Q never reach HBM.
+//   fwd_seam  per output pixel: A3 = B3 + the partial sums of the (at most
+//             2 x 2) regions whose A2 it reads, in a fixed order (no ReLU:
+//             SKIP_RELU), so the result is deterministic.
 //
-// A region chunk is one region row of 32 pixels, so a chunk's outputs are
-// contiguous in the frame.  Rows / columns past the frame are computed on
-// clamped-in-range (or don't-care) inputs and never stored.
+// A region chunk is one region row of 32 pixels.  Rows / columns past the
+// frame are computed on zero-padded inputs; they only reach outputs past the
+// frame, which are never stored.  Each (tap row dy, partial row) pair of the
+// LDS accumulator is written by exactly one chunk, so no atomics are needed.
 #include "common.hpp"
 #include "mfma.hpp"
 #include "ops.hpp"
@@ -31,8 +36,7 @@ namespace {
 
 constexpr int kFwdRW = 32;        // region width (one chunk per region row)
 constexpr int kFwdXs = 1536;      // input tile floats staged in LDS
-constexpr int kGatherTW = 32;     // L3 gather tile: 32 x 16 outputs
-constexpr int kGatherTH = 16;
+constexpr int kFwdRhMax = 28;     // region rows (LDS partial-sum accumulator bound)
 
 struct FwdGeom {
   int W, H;      // input frame
@@ -43,22 +47,26 @@ struct FwdGeom {
 };
 
 template <int N1, int N2, int F1, int F3>
-__global__ __launch_bounds__(256, 2) void fwd_l12q_kernel(
+__global__ __launch_bounds__(256, 2) void fwd_l123_kernel(
     const float* __restrict__ X, const float* __restrict__ W1, const float* __restrict__ B1,
     const float* __restrict__ W2, const float* __restrict__ B2, const float* __restrict__ W3,
-    float* __restrict__ Q, FwdGeom g) {
+    float* __restrict__ part, FwdGeom g) {
   constexpr int K1 = F1 * F1, KS1 = (K1 + 1) / 2, NT1 = N1 / 32;
   constexpr int NT2 = (N2 + 31) / 32, KS2 = N1 / 2, KC = N2 / 2;
   constexpr int K3 = F3 * F3;
   constexpr int TW = kFwdRW + F1 - 1;  // LDS row stride of the input tile
-  constexpr int TS = N1 + 1;           // per-wave transpose row (A1, then A2)
+  constexpr int TS = N1 + 1;           // per-wave transpose row (A1, A2, then Q)
+  constexpr int EW = kFwdRW + F3 - 1;  // partial-sum window width
+  constexpr int EHM = kFwdRhMax + F3 - 1;
   static_assert(K3 <= 32 && N2 <= 32 && N2 % 2 == 0, "Q tile shape");
   __shared__ float xs[kFwdXs];
   __shared__ float ts[4][32][TS];
-  __shared__ float w3s[32][N2 + 1];  // W3[tap][c] (taps >= K3 zero), padded rows
+  __shared__ float w3s[32][N2 + 1];   // W3[tap][c] (taps >= K3 zero), padded rows
+  __shared__ float accs[F3][EHM][EW];  // [dy][partial row][partial col]
 
   const int lane = mfma::lane_id(), wave = mfma::wave_id();
   const int h = lane >> 5, li = lane & 31;
+  const int EH = g.rh + F3 - 1;
 
   // B operands: W1[tap = 2s+h][32t+li], W2[c = 2s+h][32u+li], W3[tap = li][c = 2s+h]
   float w1f[KS1][NT1];
@@ -97,7 +105,7 @@ __global__ __launch_bounds__(256, 2) void fwd_l12q_kernel(
     const int crh = min(g.rh, g.oh - oy0), crw = min(kFwdRW, g.ow - ox0);
     const int th = crh + F1 - 1, tw = crw + F1 - 1;
 
-    __syncthreads();  // the previous region's readers are done with xs
+    __syncthreads();  // the previous region's readers are done with xs / accs
     const float* xsrc = X + (size_t)n * g.W * g.H + (size_t)oy0 * g.W + ox0;
     for (int i = threadIdx.x; i < th * TW; i += 256) {
       const int iy = i / TW, ix = i - iy * TW;
@@ -150,57 +158,72 @@ __global__ __launch_bounds__(256, 2) void fwd_l12q_kernel(
       f32x16 accq = zero16();
 #pragma unroll
       for (int s = 0; s < KC; s++) accq = mma(ts[wave][li][2 * s + h], w3s[li][2 * s + h], accq);
-      // Q[pixel][tap]: per register two 25-float runs (lane = tap)
-      float* qrow = Q + (((size_t)n * g.oh + oy0 + c) * g.ow + ox0) * K3;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+      // Q[pixel][tap] -> the transpose rows (lane = tap)
       if (li < K3) {
 #pragma unroll
-        for (int r = 0; r < 16; r++) {
-          const int px = crow(r, h);
-          if (px < crw) qrow[px * K3 + li] = accq[r];
+        for (int r = 0; r < 16; r++) ts[wave][crow(r, h)][li] = accq[r];
+      }
+      __builtin_amdgcn_wave_barrier();
+      // tap row dy of this chunk feeds partial row c + F3 - 1 - dy:
+      //   accs[dy][c + F3-1 - dy][e] = sum_dx Q[e - (F3-1) + dx][dy*F3 + dx]
+      for (int i = lane; i < F3 * EW; i += 64) {
+        const int dy = i / EW, e = i - dy * EW;
+        float v = 0.0f;
+#pragma unroll
+        for (int dx = 0; dx < F3; dx++) {
+          const int px = e - (F3 - 1) + dx;
+          if (px >= 0 && px < kFwdRW) v += ts[wave][px][dy * F3 + dx];
         }
+        accs[dy][c + F3 - 1 - dy][e] = v;
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_wave_barrier();
     }
+    __syncthreads();
+    // partial row pr gets tap rows dy whose chunk c = pr - (F3-1) + dy exists
+    float* dst = part + (size_t)wi * EH * EW;
+    for (int i = threadIdx.x; i < EH * EW; i += 256) {
+      const int pr = i / EW, e = i - pr * EW;
+      float v = 0.0f;
+#pragma unroll
+      for (int dy = 0; dy < F3; dy++) {
+        const int c = pr - (F3 - 1) + dy;
+        if (c >= 0 && c < crh) v += accs[dy][pr][e];
+      }
+      dst[i] = v;
+    }
   }
 }
 
+// A3[y][x] = B3 + the partials of the regions (ry, rx) in {y, y+f3-1}/rh x
+// {x, x+f3-1}/32 (ConfigBasedDataPipeline.cpp:224-238, last layer: no ReLU)
 template <int F3>
-__global__ __launch_bounds__(256, 2) void fwd_l3g_kernel(const float* __restrict__ Q,
-                                                         const float* __restrict__ B3,
-                                                         float* __restrict__ out, int ow, int oh,
-                                                         int ntx, int nty, int batch) {
-  constexpr int K3 = F3 * F3;
-  constexpr int QW = kGatherTW + F3 - 1, QH = kGatherTH + F3 - 1;
-  __shared__ float qt[QH * QW * K3];
-  const int w3 = ow - F3 + 1, h3 = oh - F3 + 1;
+__global__ __launch_bounds__(256) void fwd_seam_kernel(const float* __restrict__ part,
+                                                       const float* __restrict__ B3,
+                                                       float* __restrict__ out, FwdGeom g) {
+  constexpr int EW = kFwdRW + F3 - 1;
+  const int w3 = g.ow - F3 + 1, h3 = g.oh - F3 + 1;
+  const int EH = g.rh + F3 - 1;
   const float b3 = B3[0];
-  const int per_frame = ntx * nty;
-  for (int wi = blockIdx.x; wi < batch * per_frame; wi += gridDim.x) {
-    const int n = wi / per_frame, rr = wi - n * per_frame;
-    const int ty0 = (rr / ntx) * kGatherTH, tx0 = (rr % ntx) * kGatherTW;
-    const int qh = min(QH, oh - ty0), qw = min(QW, ow - tx0);
-    __syncthreads();
-    for (int j = 0; j < qh; j++) {  // row j of Q: qw pixels x K3 floats, contiguous
-      const float* src = Q + (((size_t)n * oh + ty0 + j) * ow + tx0) * K3;
-      for (int i = threadIdx.x; i < qw * K3; i += 256) qt[j * QW * K3 + i] = src[i];
-    }
-    __syncthreads();
-    const int tx = threadIdx.x % kGatherTW;
-#pragma unroll
-    for (int k = 0; k < 2; k++) {
-      const int ty = threadIdx.x / kGatherTW + 8 * k;
-      const int y = ty0 + ty, x = tx0 + tx;
-      if (y < h3 && x < w3) {
-        float acc = 0.0f;
-#pragma unroll
-        for (int dy = 0; dy < F3; dy++)
-#pragma unroll
-          for (int dx = 0; dx < F3; dx++)
-            acc += qt[((ty + dy) * QW + tx + dx) * K3 + dy * F3 + dx];
-        out[((size_t)n * h3 + y) * w3 + x] = acc + b3;
+  const size_t total = (size_t)g.batch * w3 * h3;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
+    const int n = (int)(i / ((size_t)w3 * h3));
+    const int rem = (int)(i - (size_t)n * w3 * h3);
+    const int y = rem / w3, x = rem - y * w3;
+    const int rya = y / g.rh, ryb = (y + F3 - 1) / g.rh;
+    const int rxa = x / kFwdRW, rxb = (x + F3 - 1) / kFwdRW;
+    const size_t fbase = (size_t)n * g.nry * g.nrx;
+    float v = 0.0f;
+    for (int ry = rya; ry <= ryb; ry++) {
+      const int pr = y - ry * g.rh + F3 - 1;
+      for (int rx = rxa; rx <= rxb; rx++) {
+        const int e = x - rx * kFwdRW + F3 - 1;
+        v += part[((fbase + (size_t)ry * g.nrx + rx) * EH + pr) * EW + e];
       }
     }
+    out[i] = v + b3;
   }
 }
 
@@ -208,43 +231,40 @@ template <int N1, int N2, int F1, int F3>
 int run_forward(const float* X, uint32_t w, uint32_t h, uint32_t batch, const float* params,
                 float* out, void* ws, size_t ws_bytes, hipStream_t s, bool query_only,
                 size_t* need) {
-  constexpr int K3 = F3 * F3;
   const int ow = (int)w - F1 + 1, oh = (int)h - F1 + 1;
   if (ow < F3 || oh < F3) return 0;
   // region rows: the input tile (32 + f1 - 1) x (rh + f1 - 1) fits the LDS tile,
   // a multiple of the 4 waves
-  int rh = (kFwdXs / (kFwdRW + F1 - 1) - (F1 - 1)) / 4 * 4;
-  if (rh <= 0) return 0;
+  int rh = std::min((kFwdXs / (kFwdRW + F1 - 1) - (F1 - 1)) / 4 * 4, kFwdRhMax);
+  if (rh < F3) return 0;
   rh = std::min(rh, oh);
-  const size_t qbytes = (size_t)batch * ow * oh * K3 * sizeof(float);
+  FwdGeom g{(int)w, (int)h, ow, oh, rh, (ow + kFwdRW - 1) / kFwdRW, (oh + rh - 1) / rh, (int)batch};
+  const long items = (long)g.batch * g.nrx * g.nry;
+  const size_t pbytes = (size_t)items * (rh + F3 - 1) * (kFwdRW + F3 - 1) * sizeof(float);
   if (query_only) {
-    *need = qbytes;
+    *need = pbytes;
     return 1;
   }
-  if (ws_bytes < qbytes)
-    return fail(SRCNN_ERR_WORKSPACE, "fused forward: workspace %zu B < %zu B", ws_bytes, qbytes);
-  float* Q = static_cast<float*>(ws);
+  if (ws_bytes < pbytes)
+    return fail(SRCNN_ERR_WORKSPACE, "fused forward: workspace %zu B < %zu B", ws_bytes, pbytes);
+  float* part = static_cast<float*>(ws);
   const float* W1 = params;
   const float* B1 = W1 + F1 * F1 * N1;
   const float* W2 = B1 + N1;
   const float* B2 = W2 + N1 * N2;
   const float* W3 = B2 + N2;
   const float* B3 = W3 + F3 * F3 * N2;
-  FwdGeom g{(int)w, (int)h, ow, oh, rh, (ow + kFwdRW - 1) / kFwdRW, (oh + rh - 1) / rh, (int)batch};
-  const long items = (long)g.batch * g.nrx * g.nry;
   {
-    SRCNN_PROFILE("fwd_l12q_mfma", s);
-    hipLaunchKernelGGL((fwd_l12q_kernel<N1, N2, F1, F3>), dim3((unsigned)std::min<long>(items, 2048)),
-                       dim3(256), 0, s, X, W1, B1, W2, B2, W3, Q, g);
+    SRCNN_PROFILE("fwd_l123_mfma", s);
+    hipLaunchKernelGGL((fwd_l123_kernel<N1, N2, F1, F3>), dim3((unsigned)std::min<long>(items, 2048)),
+                       dim3(256), 0, s, X, W1, B1, W2, B2, W3, part, g);
     SRCNN_LAUNCH_TRY();
   }
   {
-    SRCNN_PROFILE("fwd_l3_gather", s);
-    const int w3 = ow - F3 + 1, h3 = oh - F3 + 1;
-    const int ntx = (w3 + kGatherTW - 1) / kGatherTW, nty = (h3 + kGatherTH - 1) / kGatherTH;
-    const long tiles = (long)batch * ntx * nty;
-    hipLaunchKernelGGL((fwd_l3g_kernel<F3>), dim3((unsigned)std::min<long>(tiles, 4096)), dim3(256),
-                       0, s, Q, B3, out, ow, oh, ntx, nty, (int)batch);
+    SRCNN_PROFILE("fwd_l3_seam", s);
+    const long outs = (long)batch * (ow - F3 + 1) * (oh - F3 + 1);
+    hipLaunchKernelGGL((fwd_seam_kernel<F3>), dim3((unsigned)std::min<long>((outs + 255) / 256, 8192)),
+                       dim3(256), 0, s, part, B3, out, g);
     SRCNN_LAUNCH_TRY();
   }
   return 1;
