@@ -317,16 +317,11 @@ int srcnn_update_all(const srcnn_net* net, float* params, float* grads, float* m
   size_t off[6];
   srcnn_net_offsets(net, off);
   const size_t total = off[5] + 1;
-  // layer 3, 2, 1: ConfigBasedDataPipeline.cpp:325-361
-  for (int l = 2; l >= 0; l--) {
-    const size_t wo = off[2 * l], bo = off[2 * l + 1];
-    const size_t end = l == 2 ? total : off[2 * l + 2];
-    int rc = srcnn_sgd_update(params + wo, params + bo, grads + wo, grads + bo,
-                              momentum_bufs + wo, momentum_bufs + bo, momentum, wd, lr[l], batch,
-                              (uint32_t)(bo - wo), (uint32_t)(end - bo), stream);
-    if (rc) return rc;
-  }
-  return srcnn::fill(grads, 0.0f, total, srcnn::as_stream(stream));  // :353-358
+  SRCNN_REQUIRE(total < (1ull << 32), "update_all: parameter count %zu too large", total);
+  // layers 3, 2, 1 + the six zero-fills (ConfigBasedDataPipeline.cpp:325-361) in one launch;
+  // every element's arithmetic is that of srcnn_sgd_update
+  return srcnn::update_all(params, grads, momentum_bufs, off, total, lr, momentum, wd, batch,
+                           srcnn::as_stream(stream));
 }
 
 size_t srcnn_forward_workspace_bytes(const srcnn_net* net, uint32_t w, uint32_t h,

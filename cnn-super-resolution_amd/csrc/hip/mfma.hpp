@@ -24,6 +24,22 @@ __device__ __forceinline__ f32x16 mma(float a, float b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
 
+// v_mfma_f32_16x16x4_f32 (same fp32 rate, 32-cycle issue): D[16x16] += A[16x4] * B[4x16]
+//   A: lane l holds A[l&15][k = l>>4];  B: B[k = l>>4][l&15]
+//   C/D: lane l, register i holds D[4*(l>>4) + i][l&15]
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 mma16(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ f32x4 zero4() {
+  f32x4 z;
+#pragma unroll
+  for (int i = 0; i < 4; i++) z[i] = 0.0f;
+  return z;
+}
+
 __device__ __forceinline__ constexpr int crow(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
 __device__ __forceinline__ f32x16 zero16() {

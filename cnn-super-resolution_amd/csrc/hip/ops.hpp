@@ -64,6 +64,10 @@ int reduce(int mode, const float* a, const float* gt, size_t len, uint32_t gt_w,
 int sub_scalar(float* d, float v, size_t len, hipStream_t s);
 int sub_mean(float* d, size_t len, float* mean_out, void* ws, size_t ws_bytes, hipStream_t s);
 int fill(float* d, float v, size_t n, hipStream_t s);
+// update_all: the three layers' sgd_update + zero-fill of grads, one launch;
+// off = srcnn_net_offsets(), total = P
+int update_all(float* params, float* grads, float* mom, const size_t* off, size_t total,
+               const float* lr, float mu, float wd, uint32_t batch, hipStream_t s);
 int extract_luma(const uint8_t* rgba, float* luma, uint32_t w, uint32_t h, int normalize,
                  hipStream_t s);
 int swap_luma(const uint8_t* rgba, const float* nl, uint8_t* rgb, uint32_t w, uint32_t h,

@@ -254,6 +254,52 @@ int sgd_update(float* W, float* B, const float* gW, const float* gB, float* dW, 
   return SRCNN_OK;
 }
 
+// All three layers' updates and the gradient zero-fill in one launch over the
+// flat [W1|B1|W2|B2|W3|B3] buffers (ConfigBasedDataPipeline.cpp:325-361 runs
+// update_params x3 + six zero-fills).  Same arithmetic as sgd_update_kernel per
+// element; off[] = the six segment offsets, off[6] = P.
+struct UpdateSegs {
+  uint32_t off[7];
+  float lr[3];
+};
+
+__global__ void update_all_kernel(float* __restrict__ P, float* __restrict__ G,
+                                  float* __restrict__ M, UpdateSegs sg, float mu, float wd,
+                                  float batch) {
+  const uint32_t n = sg.off[6];
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    int seg = 0;
+#pragma unroll
+    for (int k = 1; k < 6; k++) seg += i >= sg.off[k];
+    const float lr = sg.lr[seg >> 1];
+    const float g = G[i];
+    if ((seg & 1) == 0) {  // weights: update_parameters.cl:14-24
+      const float w = P[i];
+      const float dw = mu * M[i] + lr * g + wd * w;
+      P[i] = w - dw / batch;
+      M[i] = dw;
+    } else {  // biases, no weight decay: update_parameters.cl:26-32
+      const float db = mu * M[i] + lr * g;
+      P[i] -= db / batch;
+      M[i] = db;
+    }
+    G[i] = 0.0f;
+  }
+}
+
+int update_all(float* params, float* grads, float* mom, const size_t* off, size_t total,
+               const float* lr, float mu, float wd, uint32_t batch, hipStream_t s) {
+  UpdateSegs sg;
+  for (int k = 0; k < 6; k++) sg.off[k] = (uint32_t)off[k];
+  sg.off[6] = (uint32_t)total;
+  for (int k = 0; k < 3; k++) sg.lr[k] = lr[k];
+  SRCNN_PROFILE("update_all", s);
+  hipLaunchKernelGGL(update_all_kernel, dim3(grid_for(total, 256, 2048)), dim3(256), 0, s, params,
+                     grads, mom, sg, mu, wd, (float)batch);
+  SRCNN_LAUNCH_TRY();
+  return SRCNN_OK;
+}
+
 // ---------------------------------------------------------------------------
 // deterministic reductions (sum.cl:35-68, squared_error.cl:36-92):
 // pass 1: fixed grid, per-block tree in LDS -> partial[block]

@@ -32,6 +32,7 @@ namespace fused {
 
 using mfma::crow;
 using mfma::f32x16;
+using mfma::f32x4;
 using mfma::mma;
 using mfma::zero16;
 
@@ -207,34 +208,54 @@ __device__ unsigned long long g_d1_timing[1024][6];
 
 // ---------------------------------------------------------------------------
 // Kernel 3: delta1 + gW2/gB2 + gW1/gB1
+//
+// Per 32-pixel chunk (one wave):
+//   delta1 = delta2 . W2^T      16x16x4 MFMA, M = pixels (2 tiles), N = n1
+//                               channels (n1/16 tiles), K = n2
+//   gW2 += A1^T . delta2        32x32x2 MFMA, M = n1, N = n2, K = pixels
+//   relu' mask of delta1        A1 from the same LDS image
+//   gW1 += Xwin^T . delta1      16x16x4 MFMA, M = taps 0..16*MT-1, N = n1,
+//                               K = pixels; delta1's C registers are the B
+//                               operand as they stand (register i of lane
+//                               group j is pixel 4j + i of the tile)
+//   the f1*f1 - 16*MT remaining taps and gB1 (= the ones row) by VALU FMAs
+//                               on the same registers
+// With f1 = 9 that is 80 MFMA taps + 1 VALU tap, where a 32-row tap tiling
+// issues 96 rows (81 taps + ones row + 14 pad): 1/6 fewer gW1 MFMA cycles.
 // ---------------------------------------------------------------------------
 template <int N1, int N2, int F1>
 __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
     const float* __restrict__ X, const float* __restrict__ A1, const float* __restrict__ D2,
     const float* __restrict__ W2, float* __restrict__ slab, Geom g) {
   constexpr int K1 = F1 * F1, NT1 = N1 / 32, NT2 = (N2 + 31) / 32;
-  constexpr int MT = (K1 + 1 + 31) / 32;  // tap tiles (+1 ones row -> gB1)
-  constexpr int KD = (N2 + 1) / 2;        // delta1 k-steps (over n)
+  constexpr int NQ = N1 / 16;             // 16-wide channel tiles
+  constexpr int MT = K1 / 16;             // 16-tap MFMA tiles
+  constexpr int KR = K1 - 16 * MT;        // taps left to the VALU
+  constexpr int KD = N2 / 4;              // delta1 k-steps (over n)
   constexpr int DS = N2 + 1;              // padded delta2 row in LDS
   constexpr int WS = N2 + 1;              // padded W2 row in LDS
+  constexpr int A1P = N1 + 4;             // padded A1 row of the LDS image
   constexpr int NW1 = K1 * N1, NW2 = N1 * N2;
   constexpr int P12 = NW1 + N1 + NW2 + N2;  // [gW1 | gB1 | gW2 | gB2]
-  constexpr int RED = (MT * NT1 + NT1 * NT2) * 16 * 64;
-  static_assert(N2 % 2 == 0, "n2 must be even");
-  constexpr int A1S = 4 * 32 * N1;        // per-wave A1 chunk staging (LDS-DMA target)
-  constexpr int D2S = 32 * DS;            // per-wave delta2 chunk image [32][DS]
-  constexpr int D2K = (D2S + 63) / 64;    // 4-byte DMA instructions per chunk
-  constexpr int D2P = 64 * D2K;           // per-wave staging stride (whole DMA instructions)
-  constexpr int LDS_MAIN = A1S + 2 * kXsMax + N1 * WS + 4 * D2P;
+  static_assert(N2 % 4 == 0 && N1 % 32 == 0 && KR <= 4, "d1 tile shape");
+  constexpr int RED1 = MT * NQ * 4 * 64, RED2 = NT1 * NT2 * 16 * 64, REDV = (KR + 1) * NQ * 64;
+  constexpr int RED = RED1 + RED2 + REDV;
+  constexpr int A1K = (32 * A1P + 255) / 256;  // 16-byte DMA instructions per A1 chunk
+  constexpr int A1S = 256 * A1K;               // per-wave A1 staging
+  constexpr int D2S = 32 * DS;                 // per-wave delta2 chunk image [32][DS]
+  constexpr int D2K = (D2S + 63) / 64;         // 4-byte DMA instructions per chunk
+  constexpr int D2P = 64 * D2K;                // per-wave staging stride (whole DMA instructions)
+  constexpr int LDS_MAIN = 4 * A1S + 2 * kXsMax + N1 * WS + 4 * D2P;
   constexpr int LDS_TOTAL = LDS_MAIN > RED ? LDS_MAIN : RED;
   __shared__ __attribute__((aligned(16))) float smem[LDS_TOTAL];
-  float* a1s = smem;                   // [4][32][N1], lane-linear DMA image of A1 rows
-  float* xsb = smem + A1S;             // [2][kXsMax]: X tile, double-buffered over samples
+  float* a1s = smem;                   // [4][32][A1P], lane-linear DMA image of A1 rows
+  float* xsb = smem + 4 * A1S;         // [2][kXsMax]: X tile, double-buffered over samples
   float* w2s = xsb + 2 * kXsMax;       // [N1][WS]: W2[c][n]
   float* d2w = w2s + N1 * WS;          // [4][32][DS]
 
   const int lane = mfma::lane_id(), wave = mfma::wave_id();
   const int h = lane >> 5, li = lane & 31;
+  const int lq = lane & 15, lg = lane >> 4;  // 16x16x4 operand row / k group
   const int npx = g.ow * g.oh;
   // (q + 0.5) / ow in fp32 is at least 0.5/ow away from an integer for the
   // pixel counts here, so the truncation is an exact q / ow
@@ -244,58 +265,61 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
     const int c = i / N2, n = i - c * N2;
     w2s[c * WS + n] = W2[i];
   }
-  // gW1 A-operand rows of this lane: taps 32m + li (tap K1 = ones -> gB1)
+  // gW1 A-operand rows of this lane: taps 16m + lq
   int toff[MT];
-  float tsel_x[MT], tsel_1[MT];  // a = X * tsel_x + tsel_1: X tap / zero row / ones row
 #pragma unroll
   for (int m = 0; m < MT; m++) {
-    const int tap = 32 * m + li;
-    toff[m] = tap < K1 ? (tap / F1) * g.W + (tap % F1) : 0;
-    tsel_x[m] = tap < K1 ? 1.0f : 0.0f;
-    tsel_1[m] = tap == K1 ? 1.0f : 0.0f;
+    const int tap = 16 * m + lq;
+    toff[m] = (tap / F1) * g.W + (tap % F1);
   }
 
-  f32x16 g1[MT][NT1], g2[NT1][NT2];
+  f32x4 g1[MT][NQ];
+  f32x16 g2[NT1][NT2];
 #pragma unroll
   for (int m = 0; m < MT; m++)
 #pragma unroll
-    for (int t = 0; t < NT1; t++) g1[m][t] = zero16();
+    for (int t = 0; t < NQ; t++) g1[m][t] = mfma::zero4();
 #pragma unroll
   for (int t = 0; t < NT1; t++)
 #pragma unroll
     for (int u = 0; u < NT2; u++) g2[t][u] = zero16();
-  float gb2[NT2];
+  float gb2[NT2], gv[KR + 1][NQ];  // gv[r < KR]: tap 16*MT + r; gv[KR]: gB1
 #pragma unroll
   for (int u = 0; u < NT2; u++) gb2[u] = 0.0f;
+#pragma unroll
+  for (int r = 0; r <= KR; r++)
+#pragma unroll
+    for (int t = 0; t < NQ; t++) gv[r][t] = 0.0f;
 
   float* d2me = d2w + wave * D2P;
+  float* a1me = a1s + wave * A1S;
   // One LDS-DMA instruction K of a chunk's operands (no registers):
-  //   K < 8:  A1 rows -> this wave's lane-linear [32][N1] image (16 B / lane)
-  //   K >= 8: delta2 rows -> this wave's padded [32][DS] image (4 B / lane;
-  //           the pad column re-reads col 0, lanes past the image write into
-  //           the staging padding)
+  //   K < A1K: A1 rows -> this wave's lane-linear [32][A1P] image (16 B / lane;
+  //            the 4-float pad of each row re-reads its first quad)
+  //   K >= A1K: delta2 rows -> this wave's padded [32][DS] image (4 B / lane;
+  //            the pad column re-reads col 0, lanes past the image write into
+  //            the staging padding)
   // Rows past the sample re-read its last row (A1: finite, and the delta2
   // rows there are zeroed in LDS before use).
-  constexpr int kA1K = 32 * N1 / 256;
-  constexpr int kDmaK = kA1K + D2K;
-  float* a1me = a1s + wave * 32 * N1;
+  constexpr int kDmaK = A1K + D2K;
 #define SRCNN_D1_DMA_K(SMP, C, K)                                                 \
   do {                                                                            \
     int l_ = lane; /* opaque: the address is formed here, never held */           \
     asm volatile("" : "+v"(l_));                                                  \
-    if ((K) < kA1K) {                                                             \
+    if ((K) < A1K) {                                                              \
       const int f_ = (K) * 256 + 4 * l_;                                          \
-      const int row_ = min((C) * 32 + f_ / N1, npx - 1);                          \
+      const int r_ = f_ / A1P, col_ = f_ - (f_ / A1P) * A1P;                      \
+      const int row_ = min((C) * 32 + r_, npx - 1);                               \
       __builtin_amdgcn_global_load_lds(                                           \
-          (const void*)(A1 + (size_t)(SMP) * npx * N1 + (row_ * N1 + (f_ % N1))), \
+          (const void*)(A1 + (size_t)(SMP) * npx * N1 + (row_ * N1 + (col_ < N1 ? col_ : 0))), \
           (__attribute__((address_space(3))) void*)(a1me + (K) * 256), 16, 0, 0); \
     } else {                                                                      \
-      const int f_ = 64 * ((K) - kA1K) + l_;                                      \
+      const int f_ = 64 * ((K) - A1K) + l_;                                       \
       const int r_ = f_ / DS, col_ = f_ - (f_ / DS) * DS;                         \
       const int row_ = min((C) * 32 + r_, npx - 1);                               \
       __builtin_amdgcn_global_load_lds(                                           \
           (const void*)(D2 + (size_t)(SMP) * npx * N2 + row_ * N2 + (col_ < N2 ? col_ : 0)), \
-          (__attribute__((address_space(3))) void*)(d2me + 64 * ((K) - kA1K)), 4, 0, 0); \
+          (__attribute__((address_space(3))) void*)(d2me + 64 * ((K) - A1K)), 4, 0, 0); \
     }                                                                             \
   } while (0)
 #define SRCNN_D1_DMA_ALL(SMP, C)                                                  \
@@ -303,12 +327,6 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
     _Pragma("unroll") for (int k_ = 0; k_ < kDmaK; k_++) SRCNN_D1_DMA_K(SMP, C, k_); \
   } while (0)
   const int nch = (npx + 31) / 32;
-  // A1[p][c] of this lane's accumulator slots, read from the LDS image at use
-#ifndef SRCNN_D1_PURE_MFMA
-#define SRCNN_D1_A1(T, R) a1me[crow(R, h) * N1 + 32 * (T) + li]
-#else  // diagnostics only: no LDS operands (results invalid)
-#define SRCNN_D1_A1(T, R) __int_as_float(crow(R, h) * N1 + 32 * (T) + li + c)
-#endif
 
 #ifdef SRCNN_D1_TIMING
   unsigned long long tacc[6] = {0, 0, 0, 0, 0, 0}, tlast = clock64();
@@ -346,8 +364,7 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
     if (has_next && wave >= nch) SRCNN_D1_X_DMA(next, xsb + (xbuf ^ 1) * kXsMax);
 
     for (int c = wave; c < nch; c += 4) {
-      // the A1 DMA of this chunk has landed (the delta2 loads above already
-      // waited for the older VM ops; keep the wait explicit for the DMA)
+      // this chunk's operand DMA has landed
       SRCNN_D1_TICK(0);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_wave_barrier();
@@ -359,27 +376,24 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
       }
 
       SRCNN_D1_TICK(1);
-      // delta1[p][c] = [A1 > 0] * sum_n delta2[p][n] * W2[c][n]  (layer_deltas.cl, f=1)
-      f32x16 d1[NT1];
+      // delta1[p][c] = sum_n delta2[p][n] * W2[c][n]  (layer_deltas.cl, f=1)
+      f32x4 d1[2][NQ];
 #pragma unroll
-      for (int t = 0; t < NT1; t++) d1[t] = zero16();
+      for (int pm = 0; pm < 2; pm++)
+#pragma unroll
+        for (int t = 0; t < NQ; t++) d1[pm][t] = mfma::zero4();
 #pragma unroll
       for (int s = 0; s < KD; s++) {
-        const int n = 2 * s + h;
-#ifndef SRCNN_D1_PURE_MFMA
-        const float a = n < N2 ? d2me[li * DS + n] : 0.0f;
-#else
-        const float a = __int_as_float(li * DS + n + c);
-#endif
+        const int n = 4 * s + lg;
+        float a[2], b[NQ];
 #pragma unroll
-        for (int t = 0; t < NT1; t++) {
-#ifndef SRCNN_D1_PURE_MFMA
-          const float b = n < N2 ? w2s[(32 * t + li) * WS + n] : 0.0f;
-#else
-          const float b = __int_as_float((32 * t + li) * WS + n);
-#endif
-          d1[t] = mma(a, b, d1[t]);
-        }
+        for (int pm = 0; pm < 2; pm++) a[pm] = d2me[(16 * pm + lq) * DS + n];
+#pragma unroll
+        for (int t = 0; t < NQ; t++) b[t] = w2s[(16 * t + lq) * WS + n];
+#pragma unroll
+        for (int pm = 0; pm < 2; pm++)
+#pragma unroll
+          for (int t = 0; t < NQ; t++) d1[pm][t] = mfma::mma16(a[pm], b[t], d1[pm][t]);
       }
       SRCNN_D1_TICK(2);
       // gW2[c][n] += sum_p A1[p][c] delta2[p][n]; gB2[n] += sum_p delta2[p][n]
@@ -389,91 +403,92 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
 #pragma unroll
         for (int u = 0; u < NT2; u++) {
           const int n = 32 * u + li;
-#ifndef SRCNN_D1_PURE_MFMA
           const float b = n < N2 ? d2me[pr * DS + n] : 0.0f;
-#else
-          const float b = __int_as_float(pr * DS + n + c);
-#endif
           gb2[u] += b;
 #pragma unroll
-          for (int t = 0; t < NT1; t++) g2[t][u] = mma(SRCNN_D1_A1(t, s), b, g2[t][u]);
+          for (int t = 0; t < NT1; t++) g2[t][u] = mma(a1me[pr * A1P + 32 * t + li], b, g2[t][u]);
         }
       }
 
       // relu' mask of delta1 (after the independent gW2 MFMAs, so the delta1
       // chain has drained without stalling the matrix core)
 #pragma unroll
-      for (int t = 0; t < NT1; t++)
+      for (int pm = 0; pm < 2; pm++)
 #pragma unroll
-        for (int r = 0; r < 16; r++) d1[t][r] = SRCNN_D1_A1(t, r) > 0.0f ? d1[t][r] : 0.0f;
+        for (int t = 0; t < NQ; t++)
+#pragma unroll
+          for (int i = 0; i < 4; i++)
+            d1[pm][t][i] = a1me[(16 * pm + 4 * lg + i) * A1P + 16 * t + lq] > 0.0f ? d1[pm][t][i] : 0.0f;
 
       SRCNN_D1_TICK(3);
-      // next chunk's A1 DMA overlaps the gW1 MFMAs (the image's reads retired)
+      // next chunk's operand DMA overlaps the gW1 MFMAs (the images' reads retired)
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
-      // gW1[tap][c] += sum_p X[p + tap] delta1[p][c]; ones row -> gB1[c].
-      // Hand-pipelined: the X gathers of step s+1 are issued before the
-      // MFMAs of step s, and the operand DMA of this wave's next work item
-      // (the next chunk, or its first chunk of the next sample, or when
-      // neither exists a harmless re-read of this one) is spread over the
-      // steps so its address math issues while the matrix core is busy.
+      // gW1[tap][c] += sum_p X[p + tap] delta1[p][c].  K-step (pm, i): lane
+      // group lg supplies pixel 16pm + 4lg + i.  Hand-pipelined: the X
+      // gathers of step s+1 are issued before the MFMAs of step s, and the
+      // operand DMA of this wave's next work item (the next chunk, or its
+      // first chunk of the next sample, or when neither exists a harmless
+      // re-read of this one) is spread over the steps.
       {
         const bool more = c + 4 < nch;
         const int dsmp = more ? sample : (has_next ? next : sample);
         const int dch = more ? c + 4 : (has_next ? wave : c);
-        // X offset of pixel row crow(s, h) of this chunk (rows past the
-        // sample clamp to its last pixel: their delta1 is 0)
-#ifndef SRCNN_D1_PURE_MFMA
-#define SRCNN_D1_XS(I) xs[I]
-#else
-#define SRCNN_D1_XS(I) __int_as_float(I)
-#endif
+        // X offset of this lane's pixel in step S (rows past the sample clamp
+        // to its last pixel: their delta1 is 0)
 #define SRCNN_D1_XB(S)                                                              \
   ([&]() {                                                                          \
-    const int q_ = min(c * 32 + crow((S), h), npx - 1);                             \
+    const int q_ = min(c * 32 + 16 * ((S) >> 2) + 4 * lg + ((S) & 3), npx - 1);    \
     const int y_ = (int)(((float)q_ + 0.5f) * inv_ow);                              \
     return q_ + y_ * (g.W - g.ow);                                                  \
   }())
-#define SRCNN_D1_GATHER(XB, M)                                                      \
-  ([&]() {                                                                          \
-    float a_ = SRCNN_D1_XS((XB) + toff[M]);                                         \
-    if (32 * (M) + 31 >= K1) a_ = tsel_x[M] != 0.0f ? a_ : tsel_1[M];               \
-    return a_;                                                                      \
-  }())
-        float acur[MT];
+        constexpr int kDmaPerStep = (kDmaK + 7) / 8;
+        float acur[MT], rcur[KR > 0 ? KR : 1];
         {
           const int xb = SRCNN_D1_XB(0);
 #pragma unroll
-          for (int m = 0; m < MT; m++) acur[m] = SRCNN_D1_GATHER(xb, m);
+          for (int m = 0; m < MT; m++) acur[m] = xs[xb + toff[m]];
+#pragma unroll
+          for (int r = 0; r < KR; r++) {
+            const int tap = 16 * MT + r;
+            rcur[r] = xs[xb + (tap / F1) * g.W + (tap % F1)];
+          }
         }
 #pragma unroll
-        for (int s = 0; s < 16; s++) {
-          float anxt[MT];
-          if (s + 1 < 16) {
+        for (int s = 0; s < 8; s++) {
+          const int pm = s >> 2, i = s & 3;
+          float anxt[MT], rnxt[KR > 0 ? KR : 1];
+          if (s + 1 < 8) {
             const int xb = SRCNN_D1_XB(s + 1);
 #pragma unroll
-            for (int m = 0; m < MT; m++) anxt[m] = SRCNN_D1_GATHER(xb, m);
+            for (int m = 0; m < MT; m++) anxt[m] = xs[xb + toff[m]];
+#pragma unroll
+            for (int r = 0; r < KR; r++) {
+              const int tap = 16 * MT + r;
+              rnxt[r] = xs[xb + (tap / F1) * g.W + (tap % F1)];
+            }
           }
 #pragma unroll
           for (int m = 0; m < MT; m++)
 #pragma unroll
-            for (int t = 0; t < NT1; t++) g1[m][t] = mma(acur[m], d1[t][s], g1[m][t]);
-#ifndef SRCNN_D1_PURE_MFMA
-          if (2 * s < kDmaK) SRCNN_D1_DMA_K(dsmp, dch, 2 * s);
-          if (2 * s + 1 < kDmaK) SRCNN_D1_DMA_K(dsmp, dch, 2 * s + 1);
-#endif
-          if (s + 1 < 16) {
+            for (int t = 0; t < NQ; t++) g1[m][t] = mfma::mma16(acur[m], d1[pm][t][i], g1[m][t]);
+#pragma unroll
+          for (int t = 0; t < NQ; t++) {
+#pragma unroll
+            for (int r = 0; r < KR; r++) gv[r][t] = fmaf(rcur[r], d1[pm][t][i], gv[r][t]);
+            gv[KR][t] += d1[pm][t][i];
+          }
+#pragma unroll
+          for (int k = 0; k < kDmaPerStep; k++)
+            if (kDmaPerStep * s + k < kDmaK) SRCNN_D1_DMA_K(dsmp, dch, kDmaPerStep * s + k);
+          if (s + 1 < 8) {
 #pragma unroll
             for (int m = 0; m < MT; m++) acur[m] = anxt[m];
+#pragma unroll
+            for (int r = 0; r < KR; r++) rcur[r] = rnxt[r];
           }
         }
-        if (32 < kDmaK) {  // more DMA instructions than two per step
-#pragma unroll
-          for (int k = 32; k < kDmaK; k++) SRCNN_D1_DMA_K(dsmp, dch, k);
-        }
 #undef SRCNN_D1_XB
-#undef SRCNN_D1_XS
-#undef SRCNN_D1_GATHER
       }
       SRCNN_D1_TICK(5);
       __builtin_amdgcn_wave_barrier();
@@ -482,7 +497,6 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
 #undef SRCNN_D1_DMA_K
 #undef SRCNN_D1_DMA_ALL
 #undef SRCNN_D1_X_DMA
-#undef SRCNN_D1_A1
 
 #ifdef SRCNN_D1_TIMING
   if (lane == 0 && wave == 0)
@@ -497,39 +511,49 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
 #pragma unroll
       for (int m = 0; m < MT; m++)
 #pragma unroll
-        for (int t = 0; t < NT1; t++, k++)
+        for (int t = 0; t < NQ; t++, k++)
 #pragma unroll
-          for (int r = 0; r < 16; r++) {
-            float* d = red + (k * 16 + r) * 64 + lane;
+          for (int r = 0; r < 4; r++) {
+            float* d = red + (k * 4 + r) * 64 + lane;
             *d = (w == 0 ? 0.0f : *d) + g1[m][t][r];
           }
+      k = 0;
 #pragma unroll
       for (int t = 0; t < NT1; t++)
 #pragma unroll
         for (int u = 0; u < NT2; u++, k++)
 #pragma unroll
           for (int r = 0; r < 16; r++) {
-            float* d = red + (k * 16 + r) * 64 + lane;
+            float* d = red + RED1 + (k * 16 + r) * 64 + lane;
             *d = (w == 0 ? 0.0f : *d) + g2[t][u][r];
           }
+#pragma unroll
+      for (int r = 0; r <= KR; r++)
+#pragma unroll
+        for (int t = 0; t < NQ; t++) {
+          float* d = red + RED1 + RED2 + (r * NQ + t) * 64 + lane;
+          *d = (w == 0 ? 0.0f : *d) + gv[r][t];
+        }
     }
     __syncthreads();
   }
   float* out = slab + (size_t)blockIdx.x * P12;
-  for (int i = threadIdx.x; i < RED; i += blockDim.x) {
+  for (int i = threadIdx.x; i < RED1; i += blockDim.x) {  // taps 0 .. 16*MT-1
+    const int k = i >> 8, r = (i >> 6) & 3, l = i & 63;
+    const int m = k / NQ, t = k - m * NQ;
+    out[(16 * m + 4 * (l >> 4) + r) * N1 + 16 * t + (l & 15)] = red[i];
+  }
+  for (int i = threadIdx.x; i < RED2; i += blockDim.x) {  // gW2
     const int k = i / 1024, r = (i >> 6) & 15, l = i & 63;
-    const int row = crow(r, l >> 5), col = l & 31;
-    if (k < MT * NT1) {
-      const int m = k / NT1, t = k - m * NT1;
-      const int tap = 32 * m + row, ch = 32 * t + col;
-      if (tap < K1) out[tap * N1 + ch] = red[i];
-      else if (tap == K1) out[NW1 + ch] = red[i];
-    } else {
-      const int kk = k - MT * NT1;
-      const int t = kk / NT2, u = kk - t * NT2;
-      const int ch = 32 * t + row, n = 32 * u + col;
-      if (n < N2) out[NW1 + N1 + ch * N2 + n] = red[i];
-    }
+    const int t = k / NT2, u = k - t * NT2;
+    const int ch = 32 * t + crow(r, l >> 5), n = 32 * u + (l & 31);
+    if (n < N2) out[NW1 + N1 + ch * N2 + n] = red[RED1 + i];
+  }
+  for (int i = threadIdx.x; i < (KR + 1) * N1; i += blockDim.x) {  // VALU taps, gB1
+    const int r = i / N1, ch = i - r * N1, t = ch >> 4;
+    const float* v = red + RED1 + RED2 + (r * NQ + t) * 64 + (ch & 15);
+    const float sum = ((v[0] + v[16]) + v[32]) + v[48];
+    out[r < KR ? (16 * MT + r) * N1 + ch : NW1 + ch] = sum;
   }
   // gB2: combine the two lane halves, then waves in order
   __syncthreads();
@@ -549,30 +573,57 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
   }
 }
 // ---------------------------------------------------------------------------
-// deterministic slab reduction: dst[i] += sum_b slab[b][i]
-// block = 64 columns x 16 rows; row r sums slabs r, r+16, ... in order, then
-// the 16 row partials are added in row order (a fixed tree: bit-reproducible)
+// deterministic slab reduction: dst[i] += sum_b slab[b][i] in a fixed order
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void slab_reduce_kernel(const float* __restrict__ slab, int nslab,
-                                                           int P, float* __restrict__ dst) {
-  __shared__ float part[16][65];
-  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int row = threadIdx.x >> 6;
+// Fixed-order sums of the per-block gradient slabs of up to three kernels in
+// one launch: blocks [first[k], first[k+1]) serve segment k, kSlabCols columns
+// each, 64 row lanes per column (enough blocks to spread over every CU).
+constexpr int kSlabCols = 16;
+constexpr int kSlabRows = 64;
+struct SlabSeg {
+  const float* slab;
+  float* dst;
+  int nslab, P;
+};
+struct SlabSegs {
+  SlabSeg seg[3];
+  int first[4];
+};
+
+__global__ __launch_bounds__(1024) void slab_reduce_kernel(SlabSegs ss) {
+  __shared__ float part[kSlabRows][kSlabCols + 1];
+  int k = 0;
+  while (k < 2 && (int)blockIdx.x >= ss.first[k + 1]) k++;
+  const SlabSeg sg = ss.seg[k];
+  const int cl = threadIdx.x % kSlabCols, row = threadIdx.x / kSlabCols;
+  const int col = ((int)blockIdx.x - ss.first[k]) * kSlabCols + cl;
   float acc = 0.0f;
-  if (col < P)
-    for (int b = row; b < nslab; b += 16) acc += slab[(size_t)b * P + col];
-  part[row][threadIdx.x & 63] = acc;
+  if (col < sg.P)
+    for (int b = row; b < sg.nslab; b += kSlabRows) acc += sg.slab[(size_t)b * sg.P + col];
+  part[row][cl] = acc;
   __syncthreads();
-  if (row == 0 && col < P) {
+  if (row == 0 && col < sg.P) {
     float t = 0.0f;
-#pragma unroll
-    for (int r = 0; r < 16; r++) t += part[r][threadIdx.x];
-    dst[col] += t;
+#pragma unroll 8
+    for (int r = 0; r < kSlabRows; r++) t += part[r][cl];
+    sg.dst[col] += t;
   }
 }
 
-static int reduce_slabs(const float* slab, int nslab, int P, float* dst, hipStream_t s) {
-  hipLaunchKernelGGL(slab_reduce_kernel, dim3((P + 63) / 64), dim3(1024), 0, s, slab, nslab, P, dst);
+static int reduce_slabs(const SlabSeg* segs, int nseg, hipStream_t s) {
+  SlabSegs ss{};
+  int blocks = 0;
+  for (int k = 0; k < 3; k++) {
+    ss.first[k] = blocks;
+    if (k < nseg) {
+      ss.seg[k] = segs[k];
+      blocks += (segs[k].P + kSlabCols - 1) / kSlabCols;
+    } else {
+      ss.seg[k] = SlabSeg{nullptr, nullptr, 0, 0};
+    }
+  }
+  ss.first[3] = blocks;
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3(blocks), dim3(1024), 0, s, ss);
   SRCNN_LAUNCH_TRY();
   return SRCNN_OK;
 }
@@ -659,9 +710,10 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   }
   {
     SRCNN_PROFILE("slab_reduce", s);
-    int rc = reduce_slabs(slab12, gd, NetT::P12, grads, s);
-    if (!rc) rc = reduce_slabs(slab3, g3, NetT::P3, grads + NetT::P12, s);
-    if (!rc && sq_err) rc = reduce_slabs(sqs, g3, 1, sq_err, s);
+    const SlabSeg segs[3] = {{slab12, grads, gd, NetT::P12},
+                             {slab3, grads + NetT::P12, g3, NetT::P3},
+                             {sqs, sq_err, g3, 1}};
+    int rc = reduce_slabs(segs, sq_err ? 3 : 2, s);
     if (rc) return rc;
   }
   return 1;
