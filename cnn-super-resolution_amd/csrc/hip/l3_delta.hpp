@@ -86,7 +86,7 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
   constexpr int NW3 = K3 * N2;      // gW3 size; slab row = NW3 + 1 (gB3)
   constexpr int NQ = N2 / 4;        // quads per A2 row
   static_assert(K3 <= 32, "taps must fit one 32-wide MFMA tile");
-  static_assert(N2 % 8 == 0 && (NQ & (NQ - 1)) == 0, "n2 must be 8 * 2^k");
+  static_assert(N2 % 8 == 0 && N2 <= 32 && (NQ & (NQ - 1)) == 0, "n2 must be 8, 16 or 32");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int npx2 = g.w2 * g.h2;
   const int nch = (npx2 + 31) / 32;
@@ -107,7 +107,10 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
   const int nq = npx2 * NQ;          // 16-byte quads per A2 tile
   const int ndma = (nq + 63) / 64;   // DMA instructions per tile (64 quads each)
 
+  // delta3 grid zero; the LDS past this sample's A2 image too, so operand
+  // reads of the rows past the sample (last chunk) always see finite values
   for (int i = tid; i < L.nd3; i += kL3Threads) d3g[i] = 0.0f;
+  for (int i = npx2 * N2 + tid; i < 2 * L.region; i += kL3Threads) smem[i] = 0.0f;
 
   // B operand of Q: W3[tap = li][c = 2s + h]
   float wq[KC];
@@ -123,9 +126,27 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
       wd[s][u] = (tap < K3 && n < N2) ? W3[tap * N2 + n] : 0.0f;
     }
   // gW3 A-operand row of this lane: tap li -> d3g offset of its window
-  const bool my_tap = li < K3;
-  const int my_off = d3off - (my_tap ? (li / F3) * g.w2 + li % F3 : 0);
+  // (lanes past the taps read a real window: their gW3 rows are discarded)
+  const int my_off = d3off - (li < K3 ? (li / F3) * g.w2 + li % F3 : 0);
   const float b3 = B3[0];
+  // Per-lane LDS offsets, so that every operand read in the chunk loops is
+  // one base register + an immediate:
+  //  qz[k]: Q A-operand A2[c*32 + li][4k + 2(s&1) + h] within the chunk
+  //         (the pixel's swizzle (li>>1) is the same for every chunk)
+  //  esw[j]: A2[c0 + 4h + rr][li] with (rr >> 1) & (NQ-1) == j (chunks start
+  //         at multiples of 32, so the swizzle depends on h and rr only)
+  //  od[s]: delta3 window offset of tap 2s + h for the delta2 A operand
+  int qz[NQ], esw[NQ], od[KS3];
+#pragma unroll
+  for (int k = 0; k < NQ; k++) {
+    qz[k] = li * N2 + 4 * (k ^ ((li >> 1) & (NQ - 1))) + h;
+    esw[k] = 4 * ((li >> 2) ^ ((k + 2 * h) & (NQ - 1))) + (li & 3);
+  }
+#pragma unroll
+  for (int s = 0; s < KS3; s++) {
+    const int tap = 2 * s + h;
+    od[s] = d3off - (tap < K3 ? (tap / F3) * g.w2 + tap % F3 : 0);
+  }
 
   f32x16 gacc[NT2];
 #pragma unroll
@@ -190,11 +211,12 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
 
     // ---- Q = A2 . W3^T per 32-pixel chunk (rows past npx2 are discarded) ----
     for (int c = wave; c < nch; c += nwaves) {
-      const int p = c * 32 + li;
       f32x16 acc = zero16();
       float av[KC];
+      const float* a2c = a2s + c * 32 * N2;
 #pragma unroll
-      for (int s = 0; s < KC; s++) av[s] = a2s[a2_at<N2>(p, 2 * s + h)];
+      for (int s = 0; s < KC; s++) av[s] = a2c[qz[s >> 1] + 2 * (s & 1)];
+      __builtin_amdgcn_sched_barrier(0);  // all operand reads in flight before the MFMAs
 #pragma unroll
       for (int s = 0; s < KC; s++) acc = mma(av[s], wq[s], acc);
       if (li < K3) {
@@ -239,59 +261,50 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
     // chunk's MFMAs, so the matrix core never waits for it ----
     //   delta2[q][n] = [A2 > 0] * sum_tap delta3(q - off(tap)) W3[tap][n]
     //   gW3[tap][n] += sum_p delta3(p - off(tap)) A2[p][n]
-    // (the d3g tail is zero for p >= npx2; the A2 row is clamped in range)
+    // gW3's pixel k-slot (s, h) is pixel c0 + crow(s, h): its B operand
+    // A2[c0 + crow(s,h)][li] is then also the relu' mask of delta2's C
+    // register s, so the epilogue reads nothing.  Rows past the sample: the
+    // d3g tail is zero (gW3) and their delta2 is not stored.
     {
       f32x16 prev[NT2];
+      float pm[16][NT2];
       int pc0 = -1;  // first pixel of the chunk whose delta2 is pending
       float* d2s = D2 + (size_t)sample * npx2 * N2;
-      // epilogue of a finished chunk: rows c0 + 4h + rr (rr = crow(r,h) - 4h)
-#define SRCNN_L3_D2_EPILOGUE(C0, ACC)                                                  \
+#define SRCNN_L3_D2_EPILOGUE(C0, ACC, MASK)                                            \
   do {                                                                                 \
-    const int q0_ = (C0) + 4 * h;                                                      \
-    float m_[16][NT2];                                                                 \
-    _Pragma("unroll") for (int r = 0; r < 16; r++)                                     \
-      _Pragma("unroll") for (int u = 0; u < NT2; u++) {                                \
-        const int rr_ = (r & 3) + 8 * (r >> 2);                                        \
-        const int pr_ = min(q0_ + rr_, npx2 - 1);                                      \
-        const int n_ = 32 * u + li;                                                    \
-        m_[r][u] = n_ < N2 ? a2s[a2_at<N2>(pr_, n_)] : 0.0f;                           \
-      }                                                                                \
-    float* dst_ = d2s + (size_t)q0_ * N2 + li;                                         \
+    float* dst_ = d2s + (size_t)((C0) + 4 * h) * N2 + li;                              \
     if ((C0) + 32 <= npx2) {                                                           \
       _Pragma("unroll") for (int r = 0; r < 16; r++)                                   \
         _Pragma("unroll") for (int u = 0; u < NT2; u++)                                \
           if (32 * u + li < N2)                                                        \
             dst_[((r & 3) + 8 * (r >> 2)) * N2 + 32 * u] =                             \
-                m_[r][u] > 0.0f ? (ACC)[u][r] : 0.0f;                                  \
+                (MASK)[r][u] > 0.0f ? (ACC)[u][r] : 0.0f;                              \
     } else {                                                                           \
       _Pragma("unroll") for (int r = 0; r < 16; r++)                                   \
         _Pragma("unroll") for (int u = 0; u < NT2; u++) {                              \
           const int rr_ = (r & 3) + 8 * (r >> 2);                                      \
-          if (q0_ + rr_ < npx2 && 32 * u + li < N2)                                    \
-            dst_[rr_ * N2 + 32 * u] = m_[r][u] > 0.0f ? (ACC)[u][r] : 0.0f;            \
+          if ((C0) + 4 * h + rr_ < npx2 && 32 * u + li < N2)                           \
+            dst_[rr_ * N2 + 32 * u] = (MASK)[r][u] > 0.0f ? (ACC)[u][r] : 0.0f;        \
         }                                                                              \
     }                                                                                  \
   } while (0)
       for (int c = wave; c < nch; c += nwaves) {
         const int c0 = c * 32;
         float ad[KS3], ag[16], bg[16][NT2];
+        const float* dc = d3g + c0 + li;
 #pragma unroll
-        for (int s = 0; s < KS3; s++) {
-          const int tap = 2 * s + h;
-          const int o = tap < K3 ? (tap / F3) * g.w2 + tap % F3 : 0;
-          ad[s] = tap < K3 ? d3g[c0 + li + d3off - o] : 0.0f;
-        }
+        for (int s = 0; s < KS3; s++) ad[s] = dc[od[s]];
+        const float* gc = d3g + c0 + 4 * h + my_off;
+        const float* a2c = a2s + (c0 + 4 * h) * N2;
 #pragma unroll
         for (int s = 0; s < 16; s++) {
-          const int p = c0 + 2 * s + h;
-          const int pb = min(p, npx2 - 1);
-          ag[s] = my_tap ? d3g[p + my_off] : 0.0f;
+          const int rr = (s & 3) + 8 * (s >> 2);
+          ag[s] = gc[rr];
 #pragma unroll
-          for (int u = 0; u < NT2; u++) {
-            const int n = 32 * u + li;
-            bg[s][u] = n < N2 ? a2s[a2_at<N2>(pb, n)] : 0.0f;
-          }
+          for (int u = 0; u < NT2; u++)
+            bg[s][u] = a2c[esw[(rr >> 1) & (NQ - 1)] + rr * N2 + 32 * u];
         }
+        __builtin_amdgcn_sched_barrier(0);  // all operand reads in flight before the MFMAs
         f32x16 acc[NT2];
 #pragma unroll
         for (int u = 0; u < NT2; u++) acc[u] = zero16();
@@ -303,12 +316,16 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
         for (int s = 0; s < 16; s++)
 #pragma unroll
           for (int u = 0; u < NT2; u++) gacc[u] = mma(ag[s], bg[s][u], gacc[u]);
-        if (pc0 >= 0) SRCNN_L3_D2_EPILOGUE(pc0, prev);
+        if (pc0 >= 0) SRCNN_L3_D2_EPILOGUE(pc0, prev, pm);
 #pragma unroll
-        for (int u = 0; u < NT2; u++) prev[u] = acc[u];
+        for (int u = 0; u < NT2; u++) {
+          prev[u] = acc[u];
+#pragma unroll
+          for (int s = 0; s < 16; s++) pm[s][u] = bg[s][u];
+        }
         pc0 = c0;
       }
-      if (pc0 >= 0) SRCNN_L3_D2_EPILOGUE(pc0, prev);
+      if (pc0 >= 0) SRCNN_L3_D2_EPILOGUE(pc0, prev, pm);
 #undef SRCNN_L3_D2_EPILOGUE
     }
     SRCNN_L3_TICK(3);

@@ -7,7 +7,7 @@ P=$R/cnn-super-resolution_amd
 name=$1; shift
 O=$P/build/variant_$name
 mkdir -p $O $P/lib/variants
-for f in runtime.cpp abi.cpp ops_generic.hip ops_fast.hip train_fused.hip; do
+for f in $(cd $P/csrc/hip && ls *.cpp *.hip); do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -fvisibility=hidden -munsafe-fp-atomics \
     -Wno-unused-result -I$R/include -I$P/csrc/hip "$@" -x hip -c $P/csrc/hip/$f -o $O/$f.o &
 done
