@@ -81,15 +81,22 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
     const float* __restrict__ A2, const float* __restrict__ T, const float* __restrict__ W3,
     const float* __restrict__ B3, float* __restrict__ D2, float* __restrict__ slab3,
     float* __restrict__ sq_slab, L3Geom g) {
-  constexpr int K3 = F3 * F3, KS3 = (K3 + 1) / 2, NT2 = (N2 + 31) / 32;
-  constexpr int KC = N2 / 2;        // Q k-steps (over channels)
-  constexpr int NW3 = K3 * N2;      // gW3 size; slab row = NW3 + 1 (gB3)
-  constexpr int NQ = N2 / 4;        // quads per A2 row
-  static_assert(K3 <= 32, "taps must fit one 32-wide MFMA tile");
-  static_assert(N2 % 8 == 0 && N2 <= 32 && (NQ & (NQ - 1)) == 0, "n2 must be 8, 16 or 32");
+  // All three GEMMs run on v_mfma_f32_16x16x4_f32 over 16-pixel units, so the
+  // ceil(npx2 / 16) units of a sample split evenly over the 8 waves (625
+  // pixels: 40 units, 5 per wave; 32-pixel chunks would leave 4 waves a third
+  // chunk while the other 4 idle).
+  constexpr int K3 = F3 * F3;
+  constexpr int TT = (K3 + 15) / 16;  // 16-wide tap tiles
+  constexpr int NT = N2 / 16;         // 16-wide channel tiles
+  constexpr int KT = (K3 + 3) / 4;    // delta2 k-steps (over taps)
+  constexpr int KQ = N2 / 4;          // Q k-steps (over channels)
+  constexpr int NW3 = K3 * N2;        // gW3 size; slab row = NW3 + 1 (gB3)
+  constexpr int NQ = N2 / 4;          // quads per A2 row
+  static_assert(K3 <= 32, "taps must fit two 16-wide MFMA tiles");
+  static_assert(N2 % 16 == 0 && N2 <= 32 && (NQ & (NQ - 1)) == 0, "n2 must be 16 or 32");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int npx2 = g.w2 * g.h2;
-  const int nch = (npx2 + 31) / 32;
+  const int nunit = (npx2 + 15) / 16;
   const L3Lds<N2, F3> L(g.w2, g.h2);
   // delta3 on the A2 grid: delta3(y, x) at d3g[(y + F3-1) * w2 + x + F3-1], zero
   // elsewhere (w3 = w2 - (F3-1), so a row's F3-1 leading columns are the zero
@@ -101,56 +108,63 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
 
   const int tid = threadIdx.x;
   const int lane = mfma::lane_id(), wave = mfma::wave_id();
-  const int h = lane >> 5, li = lane & 31;
+  const int lq = lane & 15, lg = lane >> 4;  // 16x16x4 operand row / k group
   constexpr int nwaves = kL3Threads / 64;
   const int pad = (g.W - g.w3) / 2;  // last_layer_delta.cl:25
   const int nq = npx2 * NQ;          // 16-byte quads per A2 tile
   const int ndma = (nq + 63) / 64;   // DMA instructions per tile (64 quads each)
 
   // delta3 grid zero; the LDS past this sample's A2 image too, so operand
-  // reads of the rows past the sample (last chunk) always see finite values
+  // reads of the rows past the sample (last unit) always see finite values
   for (int i = tid; i < L.nd3; i += kL3Threads) d3g[i] = 0.0f;
   for (int i = npx2 * N2 + tid; i < 2 * L.region; i += kL3Threads) smem[i] = 0.0f;
 
-  // B operand of Q: W3[tap = li][c = 2s + h]
-  float wq[KC];
+  auto tap_off = [&](int tap) { return tap < K3 ? (tap / F3) * g.w2 + tap % F3 : 0; };
+  // B operand of Q: W3[tap = 16t + lq][c = 4s + lg]
+  float wq[KQ][TT];
+  // B operand of delta2: W3[tap = 4s + lg][n = 16t + lq]
+  float wd[KT][NT];
 #pragma unroll
-  for (int s = 0; s < KC; s++) wq[s] = li < K3 ? W3[li * N2 + 2 * s + h] : 0.0f;
-  // B operand of delta2: W3[tap = 2s + h][n = 32u + li]
-  float wd[KS3][NT2];
+  for (int s = 0; s < KQ; s++)
 #pragma unroll
-  for (int s = 0; s < KS3; s++)
-#pragma unroll
-    for (int u = 0; u < NT2; u++) {
-      const int tap = 2 * s + h, n = 32 * u + li;
-      wd[s][u] = (tap < K3 && n < N2) ? W3[tap * N2 + n] : 0.0f;
+    for (int t = 0; t < TT; t++) {
+      const int tap = 16 * t + lq;
+      wq[s][t] = tap < K3 ? W3[tap * N2 + 4 * s + lg] : 0.0f;
     }
-  // gW3 A-operand row of this lane: tap li -> d3g offset of its window
-  // (lanes past the taps read a real window: their gW3 rows are discarded)
-  const int my_off = d3off - (li < K3 ? (li / F3) * g.w2 + li % F3 : 0);
+#pragma unroll
+  for (int s = 0; s < KT; s++)
+#pragma unroll
+    for (int t = 0; t < NT; t++) {
+      const int tap = 4 * s + lg;
+      wd[s][t] = tap < K3 ? W3[tap * N2 + 16 * t + lq] : 0.0f;
+    }
   const float b3 = B3[0];
-  // Per-lane LDS offsets, so that every operand read in the chunk loops is
-  // one base register + an immediate:
-  //  qz[k]: Q A-operand A2[c*32 + li][4k + 2(s&1) + h] within the chunk
-  //         (the pixel's swizzle (li>>1) is the same for every chunk)
-  //  esw[j]: A2[c0 + 4h + rr][li] with (rr >> 1) & (NQ-1) == j (chunks start
-  //         at multiples of 32, so the swizzle depends on h and rr only)
-  //  od[s]: delta3 window offset of tap 2s + h for the delta2 A operand
-  int qz[NQ], esw[NQ], od[KS3];
+  // Per-lane LDS offsets, so that every operand read in the unit loops is
+  // one base register + an immediate (units start at multiples of 16
+  // pixels, so the A2 swizzle of a unit-relative pixel is unit independent):
+  //  qz[s]:     Q A operand A2[u0 + lq][4s + lg]
+  //  bsw[t][j]: A2[u0 + 4lg + s][16t + lq] for s >> 1 == j
+  //  od[s]:     delta3 window of tap 4s + lg (delta2 A operand, pixel u0 + lq)
+  //  goff[t]:   delta3 window of tap 16t + lq (gW3 A operand; lanes past the
+  //             taps read a real window: their gW3 rows are discarded)
+  int qz[KQ], bsw[NT][2], od[KT], goff[TT];
 #pragma unroll
-  for (int k = 0; k < NQ; k++) {
-    qz[k] = li * N2 + 4 * (k ^ ((li >> 1) & (NQ - 1))) + h;
-    esw[k] = 4 * ((li >> 2) ^ ((k + 2 * h) & (NQ - 1))) + (li & 3);
-  }
+  for (int s = 0; s < KQ; s++) qz[s] = lq * N2 + 4 * (s ^ ((lq >> 1) & (NQ - 1))) + lg;
 #pragma unroll
-  for (int s = 0; s < KS3; s++) {
-    const int tap = 2 * s + h;
-    od[s] = d3off - (tap < K3 ? (tap / F3) * g.w2 + tap % F3 : 0);
-  }
+  for (int t = 0; t < NT; t++)
+#pragma unroll
+    for (int j = 0; j < 2; j++)
+      bsw[t][j] = 4 * ((4 * t + (lq >> 2)) ^ ((2 * lg + j) & (NQ - 1))) + (lq & 3);
+#pragma unroll
+  for (int s = 0; s < KT; s++) od[s] = d3off - tap_off(4 * s + lg);
+#pragma unroll
+  for (int t = 0; t < TT; t++) goff[t] = d3off - tap_off(16 * t + lq);
 
-  f32x16 gacc[NT2];
+  f32x4 gacc[TT][NT];
 #pragma unroll
-  for (int u = 0; u < NT2; u++) gacc[u] = zero16();
+  for (int t3 = 0; t3 < TT; t3++)
+#pragma unroll
+    for (int t = 0; t < NT; t++) gacc[t3][t] = mfma::zero4();
   float gb3 = 0.0f, sq = 0.0f;
 
   // A2 tile of SAMPLE -> region DST by LDS-DMA: instruction k writes image
@@ -209,21 +223,35 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
     const bool has_next = sample + (int)gridDim.x < g.batch;
     if (has_next) SRCNN_L3_T_PREFETCH(sample + gridDim.x);
 
-    // ---- Q = A2 . W3^T per 32-pixel chunk (rows past npx2 are discarded) ----
-    for (int c = wave; c < nch; c += nwaves) {
-      f32x16 acc = zero16();
-      float av[KC];
-      const float* a2c = a2s + c * 32 * N2;
+    // ---- Q = A2 . W3^T per 16-pixel unit (rows past npx2 are discarded) ----
+    for (int u = wave; u < nunit; u += nwaves) {
+      const int u0 = 16 * u;
+      const float* a2u = a2s + u0 * N2;
+      float av[KQ];
 #pragma unroll
-      for (int s = 0; s < KC; s++) av[s] = a2c[qz[s >> 1] + 2 * (s & 1)];
+      for (int s = 0; s < KQ; s++) av[s] = a2u[qz[s]];
       __builtin_amdgcn_sched_barrier(0);  // all operand reads in flight before the MFMAs
+      f32x4 acc[TT];
 #pragma unroll
-      for (int s = 0; s < KC; s++) acc = mma(av[s], wq[s], acc);
-      if (li < K3) {
+      for (int t = 0; t < TT; t++) acc[t] = mfma::zero4();
 #pragma unroll
-        for (int r = 0; r < 16; r++) {
-          const int q = c * 32 + crow(r, h);
-          if (q < npx2) qs[q * K3 + li] = acc[r];
+      for (int s = 0; s < KQ; s++)
+#pragma unroll
+        for (int t = 0; t < TT; t++) acc[t] = mfma::mma16(av[s], wq[s][t], acc[t]);
+      // Q[u0 + 4lg + i][tap = 16t + lq]
+#pragma unroll
+      for (int t = 0; t < TT; t++) {
+        const int tap = 16 * t + lq;
+        if (tap < K3) {
+          float* qd = qs + (u0 + 4 * lg) * K3 + tap;
+          if (u0 + 16 <= npx2) {
+#pragma unroll
+            for (int i = 0; i < 4; i++) qd[i * K3] = acc[t][i];
+          } else {
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+              if (u0 + 4 * lg + i < npx2) qd[i * K3] = acc[t][i];
+          }
         }
       }
     }
@@ -256,76 +284,74 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
     // Q is consumed: the next sample's A2 streams into its region meanwhile
     if (has_next) SRCNN_L3_A2_DMA(sample + gridDim.x, other);
 
-    // ---- per 32-pixel chunk: delta2 and gW3 MFMAs; the delta2 epilogue
-    // (relu' mask + store) of the PREVIOUS chunk is issued behind the current
-    // chunk's MFMAs, so the matrix core never waits for it ----
+    // ---- per 16-pixel unit: delta2 and gW3 MFMAs; the delta2 epilogue
+    // (relu' mask + store) of the PREVIOUS unit is issued behind the current
+    // unit's MFMAs, so the matrix core never waits for it ----
     //   delta2[q][n] = [A2 > 0] * sum_tap delta3(q - off(tap)) W3[tap][n]
     //   gW3[tap][n] += sum_p delta3(p - off(tap)) A2[p][n]
-    // gW3's pixel k-slot (s, h) is pixel c0 + crow(s, h): its B operand
-    // A2[c0 + crow(s,h)][li] is then also the relu' mask of delta2's C
+    // gW3's pixel k-slot (s, lg) is pixel u0 + 4lg + s: its B operand
+    // A2[u0 + 4lg + s][16t + lq] is then also the relu' mask of delta2's C
     // register s, so the epilogue reads nothing.  Rows past the sample: the
     // d3g tail is zero (gW3) and their delta2 is not stored.
     {
-      f32x16 prev[NT2];
-      float pm[16][NT2];
-      int pc0 = -1;  // first pixel of the chunk whose delta2 is pending
+      f32x4 prev[NT];
+      float pm[4][NT];
+      int pu0 = -1;  // first pixel of the unit whose delta2 is pending
       float* d2s = D2 + (size_t)sample * npx2 * N2;
-#define SRCNN_L3_D2_EPILOGUE(C0, ACC, MASK)                                            \
+#define SRCNN_L3_D2_EPILOGUE(U0, ACC, MASK)                                            \
   do {                                                                                 \
-    float* dst_ = d2s + (size_t)((C0) + 4 * h) * N2 + li;                              \
-    if ((C0) + 32 <= npx2) {                                                           \
-      _Pragma("unroll") for (int r = 0; r < 16; r++)                                   \
-        _Pragma("unroll") for (int u = 0; u < NT2; u++)                                \
-          if (32 * u + li < N2)                                                        \
-            dst_[((r & 3) + 8 * (r >> 2)) * N2 + 32 * u] =                             \
-                (MASK)[r][u] > 0.0f ? (ACC)[u][r] : 0.0f;                              \
+    float* dst_ = d2s + (size_t)((U0) + 4 * lg) * N2 + lq;                             \
+    if ((U0) + 16 <= npx2) {                                                           \
+      _Pragma("unroll") for (int i = 0; i < 4; i++)                                    \
+        _Pragma("unroll") for (int t = 0; t < NT; t++)                                 \
+          dst_[i * N2 + 16 * t] = (MASK)[i][t] > 0.0f ? (ACC)[t][i] : 0.0f;            \
     } else {                                                                           \
-      _Pragma("unroll") for (int r = 0; r < 16; r++)                                   \
-        _Pragma("unroll") for (int u = 0; u < NT2; u++) {                              \
-          const int rr_ = (r & 3) + 8 * (r >> 2);                                      \
-          if ((C0) + 4 * h + rr_ < npx2 && 32 * u + li < N2)                           \
-            dst_[rr_ * N2 + 32 * u] = (MASK)[r][u] > 0.0f ? (ACC)[u][r] : 0.0f;        \
-        }                                                                              \
+      _Pragma("unroll") for (int i = 0; i < 4; i++)                                    \
+        _Pragma("unroll") for (int t = 0; t < NT; t++)                                 \
+          if ((U0) + 4 * lg + i < npx2)                                                \
+            dst_[i * N2 + 16 * t] = (MASK)[i][t] > 0.0f ? (ACC)[t][i] : 0.0f;          \
     }                                                                                  \
   } while (0)
-      for (int c = wave; c < nch; c += nwaves) {
-        const int c0 = c * 32;
-        float ad[KS3], ag[16], bg[16][NT2];
-        const float* dc = d3g + c0 + li;
+      for (int u = wave; u < nunit; u += nwaves) {
+        const int u0 = 16 * u;
+        float ad[KT], ag[4][TT], bg[4][NT];
+        const float* dcu = d3g + u0 + lq;
 #pragma unroll
-        for (int s = 0; s < KS3; s++) ad[s] = dc[od[s]];
-        const float* gc = d3g + c0 + 4 * h + my_off;
-        const float* a2c = a2s + (c0 + 4 * h) * N2;
+        for (int s = 0; s < KT; s++) ad[s] = dcu[od[s]];
+        const float* gcu = d3g + u0 + 4 * lg;
+        const float* a2u = a2s + (u0 + 4 * lg) * N2;
 #pragma unroll
-        for (int s = 0; s < 16; s++) {
-          const int rr = (s & 3) + 8 * (s >> 2);
-          ag[s] = gc[rr];
+        for (int s = 0; s < 4; s++) {
 #pragma unroll
-          for (int u = 0; u < NT2; u++)
-            bg[s][u] = a2c[esw[(rr >> 1) & (NQ - 1)] + rr * N2 + 32 * u];
+          for (int t3 = 0; t3 < TT; t3++) ag[s][t3] = gcu[goff[t3] + s];
+#pragma unroll
+          for (int t = 0; t < NT; t++) bg[s][t] = a2u[bsw[t][s >> 1] + s * N2];
         }
         __builtin_amdgcn_sched_barrier(0);  // all operand reads in flight before the MFMAs
-        f32x16 acc[NT2];
+        f32x4 acc[NT];
 #pragma unroll
-        for (int u = 0; u < NT2; u++) acc[u] = zero16();
+        for (int t = 0; t < NT; t++) acc[t] = mfma::zero4();
 #pragma unroll
-        for (int s = 0; s < KS3; s++)
+        for (int s = 0; s < KT; s++)
 #pragma unroll
-          for (int u = 0; u < NT2; u++) acc[u] = mma(ad[s], wd[s][u], acc[u]);
+          for (int t = 0; t < NT; t++) acc[t] = mfma::mma16(ad[s], wd[s][t], acc[t]);
 #pragma unroll
-        for (int s = 0; s < 16; s++)
+        for (int s = 0; s < 4; s++)
 #pragma unroll
-          for (int u = 0; u < NT2; u++) gacc[u] = mma(ag[s], bg[s][u], gacc[u]);
-        if (pc0 >= 0) SRCNN_L3_D2_EPILOGUE(pc0, prev, pm);
+          for (int t3 = 0; t3 < TT; t3++)
 #pragma unroll
-        for (int u = 0; u < NT2; u++) {
-          prev[u] = acc[u];
+            for (int t = 0; t < NT; t++)
+              gacc[t3][t] = mfma::mma16(ag[s][t3], bg[s][t], gacc[t3][t]);
+        if (pu0 >= 0) SRCNN_L3_D2_EPILOGUE(pu0, prev, pm);
 #pragma unroll
-          for (int s = 0; s < 16; s++) pm[s][u] = bg[s][u];
+        for (int t = 0; t < NT; t++) {
+          prev[t] = acc[t];
+#pragma unroll
+          for (int s = 0; s < 4; s++) pm[s][t] = bg[s][t];
         }
-        pc0 = c0;
+        pu0 = u0;
       }
-      if (pc0 >= 0) SRCNN_L3_D2_EPILOGUE(pc0, prev, pm);
+      if (pu0 >= 0) SRCNN_L3_D2_EPILOGUE(pu0, prev, pm);
 #undef SRCNN_L3_D2_EPILOGUE
     }
     SRCNN_L3_TICK(3);
@@ -343,20 +369,23 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
   for (int w = 0; w < nwaves; w++) {
     if (wave == w) {
 #pragma unroll
-      for (int u = 0; u < NT2; u++)
+      for (int t3 = 0; t3 < TT; t3++)
 #pragma unroll
-        for (int r = 0; r < 16; r++) {
-          float* dst = red + (u * 16 + r) * 64 + lane;
-          *dst = (w == 0 ? 0.0f : *dst) + gacc[u][r];
-        }
+        for (int t = 0; t < NT; t++)
+#pragma unroll
+          for (int i = 0; i < 4; i++) {
+            float* dst = red + ((t3 * NT + t) * 4 + i) * 64 + lane;
+            *dst = (w == 0 ? 0.0f : *dst) + gacc[t3][t][i];
+          }
     }
     __syncthreads();
   }
   float* out = slab3 + (size_t)blockIdx.x * (NW3 + 1);
-  for (int i = tid; i < NT2 * 16 * 64; i += kL3Threads) {
-    const int u = i / 1024, r = (i >> 6) & 15, l = i & 63;
-    const int tap = crow(r, l >> 5), n = 32 * u + (l & 31);
-    if (tap < K3 && n < N2) out[tap * N2 + n] = red[i];
+  for (int i = tid; i < TT * NT * 4 * 64; i += kL3Threads) {
+    const int k = i >> 8, r = (i >> 6) & 3, l = i & 63;
+    const int t3 = k / NT, t = k - t3 * NT;
+    const int tap = 16 * t3 + 4 * (l >> 4) + r, n = 16 * t + (l & 15);
+    if (tap < K3) out[tap * N2 + n] = red[i];
   }
   // gB3 and squared error: per-wave shuffle trees, then waves in order
   for (int off = 32; off > 0; off >>= 1) {
