@@ -240,6 +240,60 @@ def forward_4k(S, net_t, frames=5, warmup=2, w=3840, h=2160):
             "algorithmic_gflop_per_frame": round(flops / 1e9, 2), "kernels": kernels}
 
 
+WIDE_NET = (128, 64, 9, 5, 5)
+
+
+def wide_training(S, steps=5, warmup=2, batch=4096):
+    """BASELINE.json configs[3]: the wide net (n1=128, n2=64, f2=5) trained on
+    1 GPU, 33x33 tiles, batch 4096, same step as the headline line.  Reported
+    beside it (tiles/s, per-kernel split, step roofline)."""
+    net_t = WIDE_NET
+    net = S.Net(*net_t)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    stream = torch.cuda.current_stream().cuda_stream
+    w = h = TILE
+    P = S.net_param_count(net)
+    rng = np.random.default_rng(77)
+    X, T = synthetic_batch(rng, batch, w, h)
+    Xd, Td = torch.from_numpy(X).to(dev), torch.from_numpy(T).to(dev)
+    params = torch.from_numpy(init_params(net_t, P)).to(dev)
+    grads = torch.zeros(P, dtype=torch.float32, device=dev)
+    mom = torch.zeros(P, dtype=torch.float32, device=dev)
+    nbytes = S.train_workspace_bytes(net, w, h, batch)
+    ws = torch.empty(nbytes // 4 + 64, dtype=torch.float32, device=dev)
+    lr = [1e-4, 1e-4, 1e-5]
+
+    def step():
+        S.train_fwd_bwd(net, Xd, Td, w, h, batch, params, grads, None, ws, nbytes, stream)
+        S.update_all(net, params, grads, mom, 0.9, 1e-3, lr, batch, stream)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    S.profile_reset()
+    S.profile_enable(True)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    S.profile_enable(False)
+    stats = S.profile_stats()
+    work = layer_work(net_t, w, h)
+    flops = sum(f for f, _ in work.values()) * batch
+    t_roof = sum(max(f / (PEAK_FP32_TFLOPS * 1e12), b / (PEAK_HBM_GBS * 1e9))
+                 for f, b in work.values()) * batch
+    ms = el / steps * 1e3
+    kernels = {k: {"launches_per_step": c / steps, "ms_per_step": round(t / steps, 4)}
+               for k, (c, t) in stats.items()}
+    return {"workload": "SRCNN wide n1=128 n2=64 f1=9 f2=5 f3=5, fp32 training, 33x33 tiles, "
+                        "batch %d (BASELINE.json configs[3])" % batch,
+            "tiles_s": round(batch * steps / el, 1), "ms_per_step": round(ms, 4), "steps": steps,
+            "tflops": round(flops / (ms * 1e-3) / 1e12, 2),
+            "step_roofline": {"t_roof_ms": round(t_roof * 1e3, 4), "frac": round(t_roof * 1e3 / ms, 4)},
+            "kernels": kernels}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -249,6 +303,7 @@ def main():
     ap.add_argument("--path", choices=["auto", "generic"], default="auto")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-forward", action="store_true", help="skip the 4K inference line")
+    ap.add_argument("--no-wide", action="store_true", help="skip the wide-net training line")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     # rehearsal of the N>1 path on a single-GPU box (NOT a measurement):
     # every rank on one device, gradients all-reduced over gloo
@@ -359,6 +414,8 @@ def main():
         }
         if world == 1 and not args.no_forward:
             out["forward"] = forward_4k(S, net_t)
+        if world == 1 and not args.no_wide:
+            out["wide"] = wide_training(S)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(net_t, budget_s=args.cpu_budget)
         print(json.dumps(out), flush=True)

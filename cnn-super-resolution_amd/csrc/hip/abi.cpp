@@ -243,6 +243,12 @@ size_t srcnn_train_workspace_bytes(const srcnn_net* net, uint32_t w, uint32_t h,
                                   nullptr, nullptr, nullptr, nullptr, 0, nullptr, true,
                                   &fused_need) == 1)
     g = std::max(g, fused_need);
+  size_t wide_need = 0;
+  if (fast_enabled() &&
+      srcnn::wide::train_fwd_bwd(net, nullptr, nullptr, w, h, batch, nullptr, nullptr, nullptr,
+                                 nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr, true,
+                                 &wide_need) == 1)
+    g = std::max(g, wide_need);
   return b + align_up(g);
 }
 
@@ -282,6 +288,10 @@ int srcnn_train_fwd_bwd(const srcnn_net* net, const float* X, const float* T, ui
     rc = srcnn::fused::train_fwd_bwd(net, X, T, w, h, batch, params, grads, sq_err, A1, A2, D2,
                                      static_cast<float*>(gws), gws_bytes, srcnn::as_stream(stream),
                                      false, nullptr);
+    if (rc != 0) return rc < 0 ? rc : SRCNN_OK;
+    rc = srcnn::wide::train_fwd_bwd(net, X, T, w, h, batch, params, grads, sq_err, A1, D1, A2, D2,
+                                    static_cast<float*>(gws), gws_bytes, srcnn::as_stream(stream),
+                                    false, nullptr);
     if (rc != 0) return rc < 0 ? rc : SRCNN_OK;
   }
   // forward: ConfigBasedDataPipeline.cpp:200-241

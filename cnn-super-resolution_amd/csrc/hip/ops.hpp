@@ -51,7 +51,27 @@ int train_fwd_bwd(const srcnn_net* net, const float* X, const float* T, uint32_t
 int forward(const srcnn_net* net, const float* X, uint32_t w, uint32_t h, uint32_t batch,
             const float* params, float* out, void* ws, size_t ws_bytes, hipStream_t s,
             bool query_only, size_t* need);
+// Deterministic slab reduction shared by the fused families: for every
+// segment, dst[i] += sum_{b < nslab} slab[b * P + i], summed in block order.
+constexpr int kMaxSlabSegs = 4;
+struct SlabSeg {
+  const float* slab;
+  float* dst;
+  int nslab, P;
+};
+int reduce_slabs(const SlabSeg* segs, int nseg, hipStream_t s);
 }  // namespace fused
+
+// Training step for nets with a spatial middle layer (train_wide.hip), e.g.
+// the wide config n1=128, n2=64, f1=9, f2=5, f3=5: per-stage MFMA kernels over
+// the reference-layout A1 / D1 / A2 / D2 buffers.  Same contract as
+// fused::train_fwd_bwd.
+namespace wide {
+int train_fwd_bwd(const srcnn_net* net, const float* X, const float* T, uint32_t w, uint32_t h,
+                  uint32_t batch, const float* params, float* grads, float* sq_err, float* A1,
+                  float* D1, float* A2, float* D2, float* slab, size_t slab_bytes, hipStream_t s,
+                  bool query_only, size_t* need);
+}  // namespace wide
 
 int sgd_update(float* W, float* B, const float* gW, const float* gB, float* dW, float* dB,
                float mu, float wd, float lr, uint32_t batch, uint32_t nW, uint32_t nB,

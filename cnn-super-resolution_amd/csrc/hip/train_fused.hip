@@ -575,25 +575,21 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
 // ---------------------------------------------------------------------------
 // deterministic slab reduction: dst[i] += sum_b slab[b][i] in a fixed order
 // ---------------------------------------------------------------------------
-// Fixed-order sums of the per-block gradient slabs of up to three kernels in
-// one launch: blocks [first[k], first[k+1]) serve segment k, kSlabCols columns
-// each, 64 row lanes per column (enough blocks to spread over every CU).
+// Fixed-order sums of the per-block gradient slabs of up to kMaxSlabSegs
+// kernels in one launch: blocks [first[k], first[k+1]) serve segment k,
+// kSlabCols columns each, 64 row lanes per column (enough blocks to spread
+// over every CU).  SlabSeg / reduce_slabs are declared in ops.hpp.
 constexpr int kSlabCols = 16;
 constexpr int kSlabRows = 64;
-struct SlabSeg {
-  const float* slab;
-  float* dst;
-  int nslab, P;
-};
 struct SlabSegs {
-  SlabSeg seg[3];
-  int first[4];
+  SlabSeg seg[kMaxSlabSegs];
+  int first[kMaxSlabSegs + 1];
 };
 
 __global__ __launch_bounds__(1024) void slab_reduce_kernel(SlabSegs ss) {
   __shared__ float part[kSlabRows][kSlabCols + 1];
   int k = 0;
-  while (k < 2 && (int)blockIdx.x >= ss.first[k + 1]) k++;
+  while (k < kMaxSlabSegs - 1 && (int)blockIdx.x >= ss.first[k + 1]) k++;
   const SlabSeg sg = ss.seg[k];
   const int cl = threadIdx.x % kSlabCols, row = threadIdx.x / kSlabCols;
   const int col = ((int)blockIdx.x - ss.first[k]) * kSlabCols + cl;
@@ -610,10 +606,10 @@ __global__ __launch_bounds__(1024) void slab_reduce_kernel(SlabSegs ss) {
   }
 }
 
-static int reduce_slabs(const SlabSeg* segs, int nseg, hipStream_t s) {
+int reduce_slabs(const SlabSeg* segs, int nseg, hipStream_t s) {
   SlabSegs ss{};
   int blocks = 0;
-  for (int k = 0; k < 3; k++) {
+  for (int k = 0; k < kMaxSlabSegs; k++) {
     ss.first[k] = blocks;
     if (k < nseg) {
       ss.seg[k] = segs[k];
@@ -622,7 +618,7 @@ static int reduce_slabs(const SlabSeg* segs, int nseg, hipStream_t s) {
       ss.seg[k] = SlabSeg{nullptr, nullptr, 0, 0};
     }
   }
-  ss.first[3] = blocks;
+  ss.first[kMaxSlabSegs] = blocks;
   hipLaunchKernelGGL(slab_reduce_kernel, dim3(blocks), dim3(1024), 0, s, ss);
   SRCNN_LAUNCH_TRY();
   return SRCNN_OK;

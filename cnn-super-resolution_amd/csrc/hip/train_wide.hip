@@ -1,0 +1,818 @@
+// train_wide.hip -- gfx950 training step for SRCNN nets whose middle layer is
+// spatial (f2 > 1): BASELINE.json configs[3], n1=128, n2=64, f1=9, f2=5, f3=5.
+//
+// The reference runs the same nine OpenCL kernels as for the default net
+// (ConfigBasedDataPipeline.cpp:200-323); for this net 95% of the step's FLOPs
+// are the three f2 x f2 x n1 x n2 contractions of layer 2 (forward, delta1 and
+// gW2: 180.6 MFLOP each per 33x33 tile).  Here every stage is
+// an fp32 MFMA implicit GEMM over the reference-layout (HWC) buffers:
+//
+//   prepack_w2   W2 -> two operand-ordered images (forward / flipped-transposed
+//                for delta1), one 1 KB coalesced load per wave per k-step
+//   wl1_fwd      L1 9x9x1 -> n1 + bias + ReLU (K = 81 taps, X tile in LDS)
+//   conv_mfma    L2 forward (+bias, ReLU) and delta1 = relu'(A1) * full-conv
+//                (delta2, W2^T): input channel chunks staged HBM -> LDS by
+//                LDS-DMA (double-buffered, 80-B pixel rows: conflict-free
+//                ds_read_b128), accumulators for the whole sample in registers
+//   wl3          L3 (Q trick) + last delta (reference relu' quirk) + squared
+//                error + delta2 (MFMA over taps) + gW3 / gB3 (MFMA over pixels)
+//   wgrad2       gW2 / gB2: 16x16x4 MFMA, K = pixels, per row band of a sample
+//                (A1 rows + delta2 rows in LDS), per-block slabs
+//   wgrad1       gW1 / gB1: K = pixels, a ones row gives gB1
+//   slab_reduce  fixed-order sum of the slabs into the gradient buffer
+//
+// Deterministic: static work assignment, fixed summation order, no atomics.
+#include "common.hpp"
+#include "mfma.hpp"
+#include "ops.hpp"
+
+namespace srcnn {
+namespace wide {
+
+using mfma::crow;
+using mfma::f32x16;
+using mfma::f32x4;
+using mfma::lane_id;
+using mfma::mma;
+using mfma::mma16;
+using mfma::wave_id;
+using mfma::zero16;
+using mfma::zero4;
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+// 16-B zero source for the LDS-DMA of padding / out-of-image slots
+__device__ float g_zero_src[64] = {0.0f};
+
+__device__ __forceinline__ void dma16(const float* src, float* lds_dst) {
+  __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)lds_dst, 16, 0, 0);
+}
+
+struct WGeom {
+  int w, h;    // X / T tile
+  int w1, h1;  // A1 / D1
+  int w2, h2;  // A2 / D2
+  int w3, h3;  // A3
+  int batch;
+};
+
+// ---------------------------------------------------------------------------
+// L1 forward: A1 = relu(B1 + conv9x9(X, W1))   (layer_uber_kernel.cl:36-96)
+// GEMM M = pixels (32-row tiles), N = 4 x 32 channels (one tile per wave),
+// K = 81 taps (+1 zero tap).  The k-slot pairing gives half h the taps
+// [KP*h, KP*h + KP), so every A operand is one ds_read_b32 at a per-half base
+// plus an immediate.
+// ---------------------------------------------------------------------------
+constexpr int kXS = 40;                // LDS row stride of an X tile (w, h <= kXS)
+constexpr int kXTile = kXS * (kXS + 1);  // + one zero row read by the padded tap
+
+template <int N1, int F1>
+__global__ __launch_bounds__(256) void wl1_fwd_kernel(const float* __restrict__ X,
+                                                      const float* __restrict__ W1,
+                                                      const float* __restrict__ B1,
+                                                      float* __restrict__ A1, WGeom g) {
+  static_assert(N1 == 128, "four waves x 32 output channels");
+  constexpr int NT = F1 * F1, KP = (NT + 1) / 2;
+  constexpr int Q = KP / F1, R = KP % F1;
+  __shared__ float xs[kXTile];
+  const int lane = lane_id(), wave = wave_id(), j = lane & 31, h = lane >> 5;
+  const int n = 32 * wave + j;
+  float wb[KP];
+#pragma unroll
+  for (int kp = 0; kp < KP; kp++) {
+    const int t = kp + KP * h;
+    wb[kp] = t < NT ? W1[t * N1 + n] : 0.0f;
+  }
+  const float bias = B1[n];
+  for (int i = threadIdx.x; i < kXTile; i += 256) xs[i] = 0.0f;
+  const int npx = g.w1 * g.h1, mtiles = (npx + 31) / 32;
+  // tap kp + KP (half 1) sits at one of two fixed offsets from tap kp
+  const int dA = h * (Q * kXS + R), dB = h * ((Q + 1) * kXS + R - F1);
+  for (int s = blockIdx.x; s < g.batch; s += gridDim.x) {
+    __syncthreads();
+    const float* xsrc = X + (size_t)s * g.w * g.h;
+    for (int i = threadIdx.x; i < g.w * g.h; i += 256) {
+      const int y = i / g.w;
+      xs[y * kXS + i - y * g.w] = xsrc[i];
+    }
+    __syncthreads();
+    float* dst = A1 + (size_t)s * npx * N1 + n;
+    for (int m = 0; m < mtiles; m += 2) {
+      int base[2];
+#pragma unroll
+      for (int u = 0; u < 2; u++) {
+        const int o = min(32 * (m + u) + j, npx - 1), oy = o / g.w1;
+        base[u] = oy * kXS + o - oy * g.w1;
+      }
+      f32x16 acc0 = zero16(), acc1 = zero16();
+#pragma unroll
+      for (int kp = 0; kp < KP; kp++) {
+        const int toff = (kp / F1) * kXS + kp % F1;
+        const int d = (kp % F1 + R < F1) ? dA : dB;
+        acc0 = mma(xs[base[0] + d + toff], wb[kp], acc0);
+        acc1 = mma(xs[base[1] + d + toff], wb[kp], acc1);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; r++) {
+        const int p0 = 32 * m + crow(r, h), p1 = p0 + 32;
+        if (p0 < npx) dst[(size_t)p0 * N1] = fmaxf(acc0[r] + bias, 0.0f);
+        if (p1 < npx) dst[(size_t)p1 * N1] = fmaxf(acc1[r] + bias, 0.0f);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// W2 operand images.  conv_mfma's k-step ks = (chunk, tap, g) contracts input
+// channels c = 16*chunk + 8*g + 4*half + jj (jj = MFMA slot 0..3, one
+// ds_read_b128 per lane); the B operand of that k-step for output tile nt is
+// one float4 per lane: Wimg[((nt * KS) + ks) * 64 + lane].
+//   forward: B = W2[tap][c][n]                     (n = 32 nt + j, N2 outputs)
+//   delta1:  B = W2[flip(tap)][n][c]               (n = 32 nt + j in n1, c in n2)
+// (layer_deltas.cl:83-105: delta_curr[y,x,n] = sum delta_next[y-dy,x-dx,k] W[dy,dx,n,k];
+//  as a correlation over delta_next padded by f-1 the tap is flipped.)
+// ---------------------------------------------------------------------------
+constexpr int kCC = 16;       // input channels per LDS chunk
+constexpr int kPS = kCC + 4;  // LDS floats per staged pixel (80 B rows)
+
+template <int CIN, int COUT, int F>
+__global__ void prepack_w2_kernel(const float* __restrict__ W2, float* __restrict__ Wf,
+                                  float* __restrict__ Wd) {
+  constexpr int FF = F * F, TOT = FF * CIN * COUT;
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 2 * TOT) return;
+  const bool delta = i >= TOT;
+  if (delta) i -= TOT;
+  const int jj = i & 3, lane = (i >> 2) & 63, j = lane & 31, hh = lane >> 5;
+  const int rest = i >> 8;
+  constexpr int KSC = FF * (kCC / 8);
+  if (!delta) {
+    constexpr int KS = (CIN / kCC) * KSC;
+    const int ks = rest % KS, nt = rest / KS;
+    const int chunk = ks / KSC, r2 = ks - chunk * KSC, t = r2 >> 1, gq = r2 & 1;
+    const int c = chunk * kCC + 8 * gq + 4 * hh + jj, n = 32 * nt + j;
+    Wf[i] = W2[((size_t)t * CIN + c) * COUT + n];
+  } else {
+    constexpr int KS = (COUT / kCC) * KSC;
+    const int ks = rest % KS, nt = rest / KS;
+    const int chunk = ks / KSC, r2 = ks - chunk * KSC, t = r2 >> 1, gq = r2 & 1;
+    const int dy = t / F, dx = t - (t / F) * F, tf = (F - 1 - dy) * F + (F - 1 - dx);
+    const int c = chunk * kCC + 8 * gq + 4 * hh + jj;  // delta2 channel (n2)
+    const int n = 32 * nt + j;                          // delta1 channel (n1)
+    Wd[i] = W2[((size_t)tf * CIN + n) * COUT + c];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// conv_mfma: out[s][p][n] = epi( sum_{tap, c} img_s[p + off(tap)][c] * W(tap, c, n) )
+//   forward (DELTA = false): img = A1, epi = relu(v + B2[n])   (layer_uber_kernel.cl)
+//   delta1  (DELTA = true):  img = delta2 zero-padded by F-1, W flipped and
+//                            transposed, epi = [A1 > 0] * v     (layer_deltas.cl)
+// Work item = (sample, 64 output channels).  4 waves: wave = (N tile nt of 32
+// channels, M group mg of MT 32-pixel tiles); the whole item's accumulators
+// live in registers across the K loop (CIN/16 chunks x F*F taps x 2).
+// Each chunk's image (img_w x img_h pixels x 16 channels, 80-B rows) is
+// staged by LDS-DMA into the other buffer while the current one is consumed;
+// the DMA instructions are spread over the first k-steps, issued after the
+// k-step's B load so that B waits never cover a fresh DMA.
+// ---------------------------------------------------------------------------
+constexpr int kImgMax = 960;                  // pixels of one chunk image (<= 31 x 31)
+constexpr int kImgSlack = 256;                // floats: one DMA instruction past the image
+
+struct CGeom {
+  int in_w, in_h, pad;    // unpadded input, zero border
+  int img_w, img_h;       // staged image = input + 2 pad
+  int out_w, out_h, npx;  // output
+  int batch;
+};
+
+template <int CIN, int COUT, int F, int MT, bool DELTA>
+__global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restrict__ in,
+                                                          const float* __restrict__ Wimg,
+                                                          const float* __restrict__ bias,
+                                                          const float* __restrict__ ycur,
+                                                          float* __restrict__ out, CGeom g) {
+  constexpr int NCH = CIN / kCC, FF = F * F, KSC = FF * (kCC / 8), KS = NCH * KSC;
+  constexpr int NP = COUT / 64;
+  static_assert(CIN % kCC == 0 && COUT % 64 == 0 && kCC == 16, "shape");
+  extern __shared__ float smem[];
+  const int lane = lane_id(), wave = wave_id(), j = lane & 31, h = lane >> 5;
+  const int nt = wave & 1, mg = wave >> 1;
+  const int img_px = g.img_w * g.img_h, slots = img_px * 5, kdma = (slots + 63) / 64;
+  const int buf_floats = img_px * kPS + kImgSlack;
+  const int nitems = g.batch * NP;
+  int abase[MT];
+#pragma unroll
+  for (int m = 0; m < MT; m++) {
+    const int o = min(32 * (mg * MT + m) + j, g.npx - 1), oy = o / g.out_w;
+    abase[m] = (oy * g.img_w + o - oy * g.out_w) * kPS + 4 * h;
+  }
+  // one LDS-DMA instruction k (64 slots of 16 B) of chunk c of item it
+  auto dma = [&](int it, int c, float* buf, int k) {
+    const int s = it / NP;
+    const int slot = k * 64 + lane;
+    const int pix = slot / 5, q = slot - 5 * pix;
+    const int iy = pix / g.img_w, ix = pix - iy * g.img_w;
+    const int y = iy - g.pad, x = ix - g.pad;
+    const bool ok = q < 4 && slot < slots && y >= 0 && y < g.in_h && x >= 0 && x < g.in_w;
+    const float* src =
+        ok ? in + ((size_t)(s * g.in_h + y) * g.in_w + x) * CIN + c * kCC + 4 * q : g_zero_src;
+    dma16(src, buf + k * 256);
+  };
+  float* const buf0 = smem;
+  float* const buf1 = smem + buf_floats;
+  if ((int)blockIdx.x < nitems)
+    for (int k = wave; k < kdma; k += 4) dma(blockIdx.x, 0, buf0, k);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int bsel = 0;
+  for (int it = blockIdx.x; it < nitems; it += gridDim.x) {
+    const int s = it / NP, part = it - s * NP;
+    const float4* wp = reinterpret_cast<const float4*>(Wimg) + (size_t)(part * 2 + nt) * KS * 64 + lane;
+    f32x16 acc[MT];
+#pragma unroll
+    for (int m = 0; m < MT; m++) acc[m] = zero16();
+    // B operands of taps t, t+1, t+2 (2 k-steps each) in flight
+    float4 b0[2], b1[2], b2[2];
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+      b0[q] = wp[(size_t)q * 64];
+      b1[q] = wp[(size_t)(2 + q) * 64];
+    }
+    for (int c = 0; c < NCH; c++) {
+      const float* cur = bsel ? buf1 : buf0;
+      float* nxt = bsel ? buf0 : buf1;
+      int nit = it, nc = c + 1;
+      if (nc == NCH) {
+        nit = it + gridDim.x;
+        nc = 0;
+      }
+      const bool stage = nit < nitems;
+      float4 a[MT], an[MT];
+#pragma unroll
+      for (int m = 0; m < MT; m++) a[m] = *reinterpret_cast<const float4*>(cur + abase[m]);
+#pragma unroll 1
+      for (int t = 0; t < FF; t++) {
+        const int toff = ((t / F) * g.img_w + (t % F)) * kPS;
+        const int tn = t + 1 < FF ? t + 1 : t;
+        const int toffn = ((tn / F) * g.img_w + (tn % F)) * kPS;
+        const int ksb = c * KSC + 2 * (t + 2);  // first k-step of tap t + 2
+#pragma unroll
+        for (int q = 0; q < 2; q++) b2[q] = wp[(size_t)min(ksb + q, KS - 1) * 64];
+        // this tap's share of the next chunk's DMA (issued after the B loads)
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+          const int k = wave + 4 * (2 * t + q);
+          if (stage && k < kdma) dma(nit, nc, nxt, k);
+        }
+        // k-step (t, 0): prefetch (t, 1)
+#pragma unroll
+        for (int m = 0; m < MT; m++)
+          an[m] = *reinterpret_cast<const float4*>(cur + abase[m] + toff + 8);
+#pragma unroll
+        for (int jj = 0; jj < 4; jj++)
+#pragma unroll
+          for (int m = 0; m < MT; m++) acc[m] = mma(a[m][jj], b0[0][jj], acc[m]);
+        // k-step (t, 1): prefetch (t + 1, 0)
+#pragma unroll
+        for (int m = 0; m < MT; m++)
+          a[m] = *reinterpret_cast<const float4*>(cur + abase[m] + toffn);
+#pragma unroll
+        for (int jj = 0; jj < 4; jj++)
+#pragma unroll
+          for (int m = 0; m < MT; m++) acc[m] = mma(an[m][jj], b0[1][jj], acc[m]);
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+          b0[q] = b1[q];
+          b1[q] = b2[q];
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      bsel ^= 1;
+    }
+    const int n = part * 64 + nt * 32 + j;
+    const float bn = DELTA ? 0.0f : bias[n];
+    // one 32-pixel tile at a time; the lane index is made opaque per tile so
+    // the compiler cannot hoist all 16*MT store addresses out of the item loop
+    const size_t obase = (size_t)s * g.npx * COUT + n;
+#pragma unroll
+    for (int m = 0; m < MT; m++) {
+      int hl = h;
+      asm volatile("" : "+v"(hl));
+      const int p0 = 32 * (mg * MT + m) + 4 * hl;
+#pragma unroll
+      for (int r = 0; r < 16; r++) {
+        const int pix = p0 + crow(r, 0);
+        if (pix < g.npx) {
+          const size_t idx = obase + (size_t)pix * COUT;
+          if (DELTA)
+            out[idx] = ycur[idx] > 0.0f ? acc[m][r] : 0.0f;
+          else
+            out[idx] = fmaxf(acc[m][r] + bn, 0.0f);
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// wl3: per sample
+//   1. Q[p][t] = sum_c A2[p][c] W3[t][c]      (MFMA: M = pixels, N = taps, K = n2)
+//   2. A3[o] = B3 + sum_t Q[o + off(t)][t]; delta3 = (A3 - T[o + pad]) [A3 > 0]
+//      (last_layer_delta.cl:34-48, relu' quirk kept); squared error
+//      (squared_error.cl); delta3 written into a zero-bordered grid Gd
+//   3. delta2[p][c] = [A2 > 0] sum_t Gd[p - off(t)] W3[t][c]   (MFMA, K = taps)
+//   4. gW3[t][c] += sum_p Gd[p - off(t)] A2[p][c]              (MFMA, K = pixels)
+// gW3 / gB3 / squared error accumulate in registers across the block's
+// samples and leave as one slab per block.
+// ---------------------------------------------------------------------------
+template <int N2, int F3>
+__global__ __launch_bounds__(256) void wl3_kernel(const float* __restrict__ A2,
+                                                  const float* __restrict__ T,
+                                                  const float* __restrict__ W3,
+                                                  const float* __restrict__ B3,
+                                                  float* __restrict__ D2, float* __restrict__ slab3,
+                                                  float* __restrict__ sqs, WGeom g, int qfloats) {
+  static_assert(N2 == 64 && F3 * F3 <= 32, "shape");
+  constexpr int FF = F3 * F3, KP3 = (FF + 1) / 2, P3 = FF * N2 + 1;
+  extern __shared__ float smem[];
+  float* Qs = smem;             // [npx2][FF], later the cross-wave reduction
+  float* Gd = smem + qfloats;   // [(h3 + 2(F3-1))][(w3 + 2(F3-1))]
+  __shared__ float red_s[2][4];
+  const int lane = lane_id(), wave = wave_id(), j = lane & 31, h = lane >> 5;
+  const int npx2 = g.w2 * g.h2, mt2 = (npx2 + 31) / 32, npx3 = g.w3 * g.h3;
+  const int GW = g.w3 + 2 * (F3 - 1), GH = g.h3 + 2 * (F3 - 1);
+  const int padT = (g.w - g.w3) / 2;  // last_layer_delta.cl:25 (from the width)
+  for (int i = threadIdx.x; i < GW * GH; i += 256) Gd[i] = 0.0f;
+  // step 1 B operand: W3[t = j][c = 8kk + 4h + jj]
+  float wq[8][4];
+#pragma unroll
+  for (int kk = 0; kk < 8; kk++)
+#pragma unroll
+    for (int jj = 0; jj < 4; jj++) wq[kk][jj] = j < FF ? W3[j * N2 + 8 * kk + 4 * h + jj] : 0.0f;
+  // step 3: wave = (N tile nt, M group mg); taps kp + KP3*h
+  const int nt = wave & 1, mg = wave >> 1;
+  float wd[KP3];
+  int goff[KP3];
+#pragma unroll
+  for (int kp = 0; kp < KP3; kp++) {
+    const int t = kp + KP3 * h, tc = min(t, FF - 1);
+    wd[kp] = t < FF ? W3[t * N2 + 32 * nt + j] : 0.0f;
+    goff[kp] = -((tc / F3) * GW + tc % F3);
+  }
+  // step 4: row = tap j
+  const int tA = min(j, FF - 1);
+  const int goffA = -((tA / F3) * GW + tA % F3);
+  const bool tapA = j < FF;
+  f32x16 gacc0 = zero16(), gacc1 = zero16();
+  float sq = 0.0f, gb3 = 0.0f;
+  const float b3 = B3[0];
+  for (int s = blockIdx.x; s < g.batch; s += gridDim.x) {
+    const float* a2s = A2 + (size_t)s * npx2 * N2;
+    __syncthreads();  // previous sample's Gd / Qs readers are done
+    // 1. Q
+    for (int mt = wave; mt < mt2; mt += 4) {
+      const int p = min(32 * mt + j, npx2 - 1);
+      const float4* src = reinterpret_cast<const float4*>(a2s + (size_t)p * N2) + h;
+      float4 v[8];
+#pragma unroll
+      for (int kk = 0; kk < 8; kk++) v[kk] = src[2 * kk];
+      f32x16 acc = zero16();
+#pragma unroll
+      for (int kk = 0; kk < 8; kk++)
+#pragma unroll
+        for (int jj = 0; jj < 4; jj++) acc = mma(v[kk][jj], wq[kk][jj], acc);
+#pragma unroll
+      for (int r = 0; r < 16; r++) {
+        const int pix = 32 * mt + crow(r, h);
+        if (pix < npx2 && j < FF) Qs[pix * FF + j] = acc[r];
+      }
+    }
+    __syncthreads();
+    // 2. A3, last delta, squared error
+    const float* ts = T + (size_t)s * g.w * g.h;
+    for (int o = threadIdx.x; o < npx3; o += 256) {
+      const int oy = o / g.w3, ox = o - oy * g.w3;
+      const float* q0 = Qs + (oy * g.w2 + ox) * FF;
+      float v = 0.0f;
+#pragma unroll
+      for (int t = 0; t < FF; t++) v += q0[((t / F3) * g.w2 + t % F3) * FF + t];
+      const float a3 = v + b3;
+      const float diff = a3 - ts[(oy + padT) * g.w + ox + padT];
+      const float d = a3 > 0.0f ? diff : 0.0f;
+      sq += diff * diff;
+      gb3 += d;
+      Gd[(oy + F3 - 1) * GW + ox + F3 - 1] = d;
+    }
+    __syncthreads();
+    // 3. delta2
+    for (int mt = mg; mt < mt2; mt += 2) {
+      const int p = min(32 * mt + j, npx2 - 1), py = p / g.w2, px = p - py * g.w2;
+      const int gb = (py + F3 - 1) * GW + px + F3 - 1;
+      f32x16 acc = zero16();
+#pragma unroll
+      for (int kp = 0; kp < KP3; kp++) acc = mma(Gd[gb + goff[kp]], wd[kp], acc);
+#pragma unroll
+      for (int r = 0; r < 16; r++) {
+        const int pix = 32 * mt + crow(r, h);
+        if (pix < npx2) {
+          const size_t idx = ((size_t)s * npx2 + pix) * N2 + 32 * nt + j;
+          D2[idx] = A2[idx] > 0.0f ? acc[r] : 0.0f;
+        }
+      }
+    }
+    // 4. gW3 (K = pixel pairs split over the waves; B columns: channel 2j + tile)
+    for (int kp = wave; 2 * kp < npx2; kp += 4) {
+      const int pk = 2 * kp + h;
+      const bool pok = pk < npx2;
+      const int p = pok ? pk : npx2 - 1, py = p / g.w2, px = p - py * g.w2;
+      const float av = Gd[(py + F3 - 1) * GW + px + F3 - 1 + goffA];
+      const float a = (tapA && pok) ? av : 0.0f;
+      const float2 bv = *reinterpret_cast<const float2*>(a2s + (size_t)p * N2 + 2 * j);
+      gacc0 = mma(a, bv.x, gacc0);
+      gacc1 = mma(a, bv.y, gacc1);
+    }
+  }
+  // cross-wave reduction of gW3 (fixed order), gB3, squared error
+  __syncthreads();
+  float* red = Qs;  // 4 waves x 2 tiles x 16 regs x 64 lanes
+#pragma unroll
+  for (int r = 0; r < 16; r++) {
+    red[((wave * 2 + 0) * 16 + r) * 64 + lane] = gacc0[r];
+    red[((wave * 2 + 1) * 16 + r) * 64 + lane] = gacc1[r];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    sq += __shfl_down(sq, o, 64);
+    gb3 += __shfl_down(gb3, o, 64);
+  }
+  if (lane == 0) {
+    red_s[0][wave] = sq;
+    red_s[1][wave] = gb3;
+  }
+  __syncthreads();
+  float* out = slab3 + (size_t)blockIdx.x * P3;
+  for (int e = threadIdx.x; e < 2 * 16 * 64; e += 256) {
+    const int tile = e / (16 * 64), r = (e / 64) % 16, l = e & 63;
+    const int tap = crow(r, l >> 5), c = 2 * (l & 31) + tile;
+    float v = 0.0f;
+    for (int w = 0; w < 4; w++) v += red[((w * 2 + tile) * 16 + r) * 64 + l];
+    if (tap < FF) out[tap * N2 + c] = v;
+  }
+  if (threadIdx.x == 0) {
+    out[FF * N2] = red_s[1][0] + red_s[1][1] + red_s[1][2] + red_s[1][3];
+    sqs[blockIdx.x] = red_s[0][0] + red_s[0][1] + red_s[0][2] + red_s[0][3];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// wgrad2: gW2[t][c][n] += sum_{s,p} A1[p + off(t)][c] delta2[p][n]; gB2[n] += sum delta2
+// (backpropagate.cl:64-113, summed race-free).  16x16x4 MFMA: rows = 16
+// channels, cols = 16 n, K = 4 pixels.  Block = (32-channel chunk cq, sample
+// group); 8 waves = (16-channel half ct) x (n tile nt), each holding all F*F
+// taps (F*F x 4 accumulators).  Per sample, bands of R output rows: the A1
+// rows they read (R + F - 1 rows x 32 channels, 48-float pixels) and their
+// delta2 rows (64 channels, 80-float pixels) are DMA'd into LDS, double
+// buffered across bands; the compute loop only reads LDS.
+// ---------------------------------------------------------------------------
+constexpr int kGAS = 48;      // LDS floats per A1 pixel (32 channels + pad)
+constexpr int kGDS = 80;      // LDS floats per delta2 pixel (64 channels + pad)
+constexpr int kBandPx = 64;   // output pixels per band (16 quads)
+constexpr int kGAPx = 192;    // A1 pixels per band image (max)
+constexpr int kGAFl = kGAPx * kGAS;
+constexpr int kGBuf = kGAFl + (kBandPx + 4) * kGDS + 256;
+
+struct G2Geom {
+  int w1, h1, w2, h2;
+  int rows, nbands;  // output rows per band, bands per sample
+  int batch, groups;
+};
+
+template <int CIN, int COUT, int F>
+__global__ __launch_bounds__(512, 1) void wgrad2_kernel(const float* __restrict__ A1,
+                                                       const float* __restrict__ D2,
+                                                       float* __restrict__ slab2, G2Geom g) {
+  static_assert(CIN % 32 == 0 && COUT == 64, "shape");
+  constexpr int FF = F * F, NCQ = CIN / 32;
+  constexpr size_t P2 = (size_t)FF * CIN * COUT + COUT;
+  extern __shared__ float smem[];
+  const int lane = lane_id(), wave = wave_id(), i = lane & 15, gq = lane >> 4;
+  const int ct = wave & 1, nt = wave >> 1;
+  const int cq = blockIdx.x % NCQ, grp = blockIdx.x / NCQ;
+  const bool gbw = cq == 0 && ct == 0;
+  f32x4 acc[FF];
+#pragma unroll
+  for (int t = 0; t < FF; t++) acc[t] = zero4();
+  float gb = 0.0f;
+  int abase[16];
+  const int bandpx_full = g.rows * g.w2;
+#pragma unroll
+  for (int kq = 0; kq < 16; kq++) {
+    const int k = min(4 * kq + gq, bandpx_full - 1), ky = k / g.w2, kx = k - ky * g.w2;
+    abase[kq] = (ky * g.w1 + kx) * kGAS + 16 * ct + i;
+  }
+  const int dlane = kGAFl + gq * kGDS + 16 * nt + i;
+  for (int e = threadIdx.x; e < 2 * kGBuf; e += 512) smem[e] = 0.0f;
+  __syncthreads();
+  // units = (sample, band) of this group
+  const int nsamp = g.batch > grp ? (g.batch - grp + g.groups - 1) / g.groups : 0;
+  const int nunits = nsamp * g.nbands;
+  auto stage = [&](int u, float* buf) {
+    const int s = grp + (u / g.nbands) * g.groups, b = u % g.nbands;
+    const int y0 = b * g.rows, rb = min(g.rows, g.h2 - y0);
+    const int apx = (rb + F - 1) * g.w1, aslots = apx * 12;
+    const float* asrc = A1 + ((size_t)s * g.h1 * g.w1 + (size_t)y0 * g.w1) * CIN + 32 * cq;
+    for (int k = wave; k * 64 < aslots; k += 8) {
+      const int slot = k * 64 + lane, pix = slot / 12, q = slot - 12 * pix;
+      const bool ok = q < 8 && slot < aslots;
+      dma16(ok ? asrc + (size_t)pix * CIN + 4 * q : g_zero_src, buf + k * 256);
+    }
+    const int dpx = rb * g.w2, dslots = (kBandPx + 4) * 20;
+    const float* dsrc = D2 + ((size_t)s * g.h2 * g.w2 + (size_t)y0 * g.w2) * COUT;
+    for (int k = wave; k * 64 < dslots; k += 8) {
+      const int slot = k * 64 + lane, pix = slot / 20, q = slot - 20 * pix;
+      const bool ok = q < 16 && pix < dpx;
+      dma16(ok ? dsrc + (size_t)pix * COUT + 4 * q : g_zero_src, buf + kGAFl + k * 256);
+    }
+  };
+  int bsel = 0;
+  if (nunits > 0) stage(0, smem);
+  for (int u = 0; u < nunits; u++) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // unit u landed; everyone is done with the other buffer
+    const float* cur = smem + (bsel ? kGBuf : 0);
+    if (u + 1 < nunits) stage(u + 1, smem + (bsel ? 0 : kGBuf));
+#pragma unroll
+    for (int kq = 0; kq < 16; kq++) {
+      const float b = cur[dlane + kq * 4 * kGDS];
+      if (gbw) gb += b;
+#pragma unroll
+      for (int t = 0; t < FF; t++) {
+        const float a = cur[abase[kq] + ((t / F) * g.w1 + t % F) * kGAS];
+        acc[t] = mma16(a, b, acc[t]);
+      }
+    }
+    bsel ^= 1;
+  }
+  // slab rows of this block: channels 32 cq + 16 ct + 4 gq + r, n = 16 nt + i
+  float* out = slab2 + (size_t)grp * P2;
+#pragma unroll
+  for (int t = 0; t < FF; t++)
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int c = 32 * cq + 16 * ct + 4 * gq + r;
+      out[((size_t)t * CIN + c) * COUT + 16 * nt + i] = acc[t][r];
+    }
+  if (gbw) {
+    gb += __shfl_down(gb, 32, 64);
+    gb += __shfl_down(gb, 16, 64);
+    if (gq == 0) out[(size_t)FF * CIN * COUT + 16 * nt + i] = gb;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// wgrad1: gW1[t][c] += sum_{s,q} X[q + off(t)] delta1[q][c]; gB1[c] += sum delta1
+// GEMM rows = 81 taps + a ones row (gB1) padded to 3 x 32, cols = 128 channels
+// as 4 tiles (column j of tile ct = channel 4j + ct: one float4 load per lane
+// feeds all four), K = pixel pairs split over the 4 waves.
+// ---------------------------------------------------------------------------
+template <int N1, int F1>
+__global__ __launch_bounds__(256) void wgrad1_kernel(const float* __restrict__ X,
+                                                     const float* __restrict__ D1,
+                                                     float* __restrict__ slab1, WGeom g) {
+  static_assert(N1 == 128, "4 column tiles of 32 x float4");
+  constexpr int NT = F1 * F1, TT = (NT + 1 + 31) / 32;
+  constexpr int P1 = NT * N1 + N1;
+  __shared__ float xs[kXTile];
+  extern __shared__ float red[];  // [TT*32][N1] cross-wave reduction
+  const int lane = lane_id(), wave = wave_id(), j = lane & 31, h = lane >> 5;
+  int toffx[TT];
+  float fill[TT];
+  bool valid[TT];
+#pragma unroll
+  for (int tt = 0; tt < TT; tt++) {
+    const int tap = 32 * tt + j, tc = min(tap, NT - 1);
+    valid[tt] = tap < NT;
+    fill[tt] = tap == NT ? 1.0f : 0.0f;
+    toffx[tt] = (tc / F1) * kXS + tc % F1;
+  }
+  f32x16 acc[TT][4];
+#pragma unroll
+  for (int tt = 0; tt < TT; tt++)
+#pragma unroll
+    for (int ct = 0; ct < 4; ct++) acc[tt][ct] = zero16();
+  for (int i = threadIdx.x; i < kXTile; i += 256) xs[i] = 0.0f;
+  const int npx = g.w1 * g.h1;
+  for (int s = blockIdx.x; s < g.batch; s += gridDim.x) {
+    __syncthreads();
+    const float* xsrc = X + (size_t)s * g.w * g.h;
+    for (int i = threadIdx.x; i < g.w * g.h; i += 256) {
+      const int y = i / g.w;
+      xs[y * kXS + i - y * g.w] = xsrc[i];
+    }
+    __syncthreads();
+    const float4* dsrc = reinterpret_cast<const float4*>(D1 + (size_t)s * npx * N1) + j;
+    for (int kp = wave; 2 * kp < npx; kp += 4) {
+      const int pk = 2 * kp + h;
+      const bool pok = pk < npx;
+      const int p = pok ? pk : npx - 1, py = p / g.w1, px = p - py * g.w1;
+      float4 b = dsrc[(size_t)p * (N1 / 4)];
+      if (!pok) b = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      const int xb = py * kXS + px;
+#pragma unroll
+      for (int tt = 0; tt < TT; tt++) {
+        const float av = xs[xb + toffx[tt]];
+        const float a = valid[tt] ? av : fill[tt];
+        acc[tt][0] = mma(a, b.x, acc[tt][0]);
+        acc[tt][1] = mma(a, b.y, acc[tt][1]);
+        acc[tt][2] = mma(a, b.z, acc[tt][2]);
+        acc[tt][3] = mma(a, b.w, acc[tt][3]);
+      }
+    }
+  }
+  // fixed-order cross-wave sum: wave 0 stores, waves 1..3 add in turn
+  for (int w = 0; w < 4; w++) {
+    __syncthreads();
+    if (wave == w) {
+#pragma unroll
+      for (int tt = 0; tt < TT; tt++)
+#pragma unroll
+        for (int ct = 0; ct < 4; ct++)
+#pragma unroll
+          for (int r = 0; r < 16; r++) {
+            const int row = 32 * tt + crow(r, h), col = 4 * j + ct;
+            float* d = red + row * N1 + col;
+            *d = w == 0 ? acc[tt][ct][r] : *d + acc[tt][ct][r];
+          }
+    }
+  }
+  __syncthreads();
+  float* out = slab1 + (size_t)blockIdx.x * P1;
+  for (int e = threadIdx.x; e < (NT + 1) * N1; e += 256) out[e] = red[e];
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+template <int N1, int N2, int F1, int F2, int F3>
+struct Net {
+  static constexpr int W1 = F1 * F1 * N1, P1 = W1 + N1;
+  static constexpr int W2 = F2 * F2 * N1 * N2, P2 = W2 + N2;
+  static constexpr int W3 = F3 * F3 * N2, P3 = W3 + 1;
+  static constexpr int MT2 = 7;   // L2 forward: up to 2 x 7 x 32 = 448 output pixels
+  static constexpr int MT4 = 10;  // delta1: up to 640 pixels
+};
+
+static size_t align_f(size_t n) { return (n + 63) & ~(size_t)63; }
+
+template <typename K>
+static int set_lds(K kernel, size_t bytes) {
+  if (bytes <= 64 * 1024) return SRCNN_OK;
+  hipError_t e = hipFuncSetAttribute((const void*)kernel,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  if (e != hipSuccess)
+    return fail(SRCNN_ERR_HIP, "hipFuncSetAttribute(%zu B LDS): %s", bytes, hipGetErrorString(e));
+  return SRCNN_OK;
+}
+
+template <int N1, int N2, int F1, int F2, int F3>
+static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t batch,
+               const float* params, float* grads, float* sq_err, float* A1, float* D1, float* A2,
+               float* D2, float* slab, size_t slab_bytes, hipStream_t s, bool query_only,
+               size_t* need) {
+  using NetT = Net<N1, N2, F1, F2, F3>;
+  WGeom g;
+  g.w = (int)w;
+  g.h = (int)h;
+  g.w1 = g.w - F1 + 1;
+  g.h1 = g.h - F1 + 1;
+  g.w2 = g.w1 - F2 + 1;
+  g.h2 = g.h1 - F2 + 1;
+  g.w3 = g.w2 - F3 + 1;
+  g.h3 = g.h2 - F3 + 1;
+  g.batch = (int)batch;
+  if (g.w > kXS || g.h > kXS || g.w3 <= 0 || g.h3 <= 0) return 0;
+  const int npx1 = g.w1 * g.h1, npx2 = g.w2 * g.h2;
+  // L2 forward / delta1 geometry limits (register tiles, LDS images)
+  CGeom cf{g.w1, g.h1, 0, g.w1, g.h1, g.w2, g.h2, npx2, g.batch};
+  CGeom cd{g.w2, g.h2, F2 - 1, g.w2 + 2 * (F2 - 1), g.h2 + 2 * (F2 - 1), g.w1, g.h1, npx1, g.batch};
+  if ((npx2 + 31) / 32 > 2 * NetT::MT2 || (npx1 + 31) / 32 > 2 * NetT::MT4) return 0;
+  if (cf.img_w * cf.img_h > kImgMax || cd.img_w * cd.img_h > kImgMax) return 0;
+  // wgrad2 bands
+  G2Geom g2;
+  g2.w1 = g.w1;
+  g2.h1 = g.h1;
+  g2.w2 = g.w2;
+  g2.h2 = g.h2;
+  g2.rows = std::min(8, kBandPx / g.w2);
+  if (g2.rows < 1 || (g2.rows + F2 - 1) * g.w1 > kGAPx) return 0;
+  g2.nbands = (g.h2 + g2.rows - 1) / g2.rows;
+  g2.batch = g.batch;
+  g2.groups = (int)std::min<uint32_t>(batch, 64);
+  // wl3 LDS
+  const int qfloats = std::max(npx2 * F3 * F3, 2 * 16 * 64 * 4);
+  const size_t lds3 = (size_t)(qfloats + (g.w3 + 2 * (F3 - 1)) * (g.h3 + 2 * (F3 - 1))) * 4;
+  if (lds3 > 64 * 1024) return 0;
+  const int G1 = (int)std::min<uint32_t>(batch, 512);
+  const int G3 = (int)std::min<uint32_t>(batch, 512);
+  const int GC = 256;
+  const int G2 = g2.groups * (N1 / 32);
+  // workspace: Wf | Wd | slab1 | slab2 | slab3 | sqs
+  const size_t nWf = align_f(NetT::W2), nWd = align_f(NetT::W2);
+  const size_t n1 = align_f((size_t)G1 * NetT::P1), n2 = align_f((size_t)g2.groups * NetT::P2);
+  const size_t n3 = align_f((size_t)G3 * NetT::P3), nsq = align_f(G3);
+  const size_t bytes = (nWf + nWd + n1 + n2 + n3 + nsq) * sizeof(float);
+  if (query_only) {
+    *need = bytes;
+    return 1;
+  }
+  if (slab_bytes < bytes)
+    return fail(SRCNN_ERR_WORKSPACE, "wide train step: workspace %zu B < %zu B", slab_bytes, bytes);
+  float* Wf = slab;
+  float* Wd = Wf + nWf;
+  float* slab1 = Wd + nWd;
+  float* slab2 = slab1 + n1;
+  float* slab3 = slab2 + n2;
+  float* sqs = slab3 + n3;
+  const float* W1 = params;
+  const float* B1 = W1 + NetT::W1;
+  const float* W2 = B1 + N1;
+  const float* B2 = W2 + NetT::W2;
+  const float* W3 = B2 + N2;
+  const float* B3 = W3 + NetT::W3;
+  {
+    SRCNN_PROFILE("wide_prepack_w2", s);
+    const int tot = 2 * NetT::W2;
+    hipLaunchKernelGGL((prepack_w2_kernel<N1, N2, F2>), dim3((tot + 255) / 256), dim3(256), 0, s,
+                       W2, Wf, Wd);
+    SRCNN_LAUNCH_TRY();
+  }
+  {
+    SRCNN_PROFILE("wide_l1_fwd", s);
+    hipLaunchKernelGGL((wl1_fwd_kernel<N1, F1>), dim3(std::min<uint32_t>(batch, 1024)), dim3(256),
+                       0, s, X, W1, B1, A1, g);
+    SRCNN_LAUNCH_TRY();
+  }
+  {
+    SRCNN_PROFILE("wide_l2_fwd", s);
+    const size_t lds = 2 * ((size_t)cf.img_w * cf.img_h * kPS + kImgSlack) * sizeof(float);
+    if (int rc = set_lds(conv_mfma_kernel<N1, N2, F2, NetT::MT2, false>, lds)) return rc;
+    const int items = g.batch * (N2 / 64);
+    hipLaunchKernelGGL((conv_mfma_kernel<N1, N2, F2, NetT::MT2, false>), dim3(std::min(items, GC)), dim3(256), lds, s, A1, Wf, B2,
+                       (const float*)nullptr, A2, cf);
+    SRCNN_LAUNCH_TRY();
+  }
+  {
+    SRCNN_PROFILE("wide_l3_delta", s);
+    if (int rc = set_lds(wl3_kernel<N2, F3>, lds3)) return rc;
+    hipLaunchKernelGGL((wl3_kernel<N2, F3>), dim3(G3), dim3(256), lds3, s, A2, T, W3, B3, D2,
+                       slab3, sqs, g, qfloats);
+    SRCNN_LAUNCH_TRY();
+  }
+  {
+    SRCNN_PROFILE("wide_delta1", s);
+    const size_t lds = 2 * ((size_t)cd.img_w * cd.img_h * kPS + kImgSlack) * sizeof(float);
+    if (int rc = set_lds(conv_mfma_kernel<N2, N1, F2, NetT::MT4, true>, lds)) return rc;
+    const int items = g.batch * (N1 / 64);
+    hipLaunchKernelGGL((conv_mfma_kernel<N2, N1, F2, NetT::MT4, true>), dim3(std::min(items, GC)), dim3(256), lds, s, D2, Wd,
+                       (const float*)nullptr, A1, D1, cd);
+    SRCNN_LAUNCH_TRY();
+  }
+  {
+    SRCNN_PROFILE("wide_grad2", s);
+    const size_t lds = 2 * (size_t)kGBuf * sizeof(float);
+    if (int rc = set_lds(wgrad2_kernel<N1, N2, F2>, lds)) return rc;
+    hipLaunchKernelGGL((wgrad2_kernel<N1, N2, F2>), dim3(G2), dim3(512), lds, s, A1, D2, slab2, g2);
+    SRCNN_LAUNCH_TRY();
+  }
+  {
+    SRCNN_PROFILE("wide_grad1", s);
+    const size_t lds = (size_t)((F1 * F1 + 1 + 31) / 32 * 32) * N1 * sizeof(float);
+    if (int rc = set_lds(wgrad1_kernel<N1, F1>, lds)) return rc;
+    hipLaunchKernelGGL((wgrad1_kernel<N1, F1>), dim3(G1), dim3(256), lds, s, X, D1, slab1, g);
+    SRCNN_LAUNCH_TRY();
+  }
+  {
+    SRCNN_PROFILE("slab_reduce", s);
+    const fused::SlabSeg segs[4] = {{slab1, grads, G1, NetT::P1},
+                                    {slab2, grads + NetT::P1, g2.groups, NetT::P2},
+                                    {slab3, grads + NetT::P1 + NetT::P2, G3, NetT::P3},
+                                    {sqs, sq_err, G3, 1}};
+    if (int rc = fused::reduce_slabs(segs, sq_err ? 4 : 3, s)) return rc;
+  }
+  return 1;
+}
+
+int train_fwd_bwd(const srcnn_net* net, const float* X, const float* T, uint32_t w, uint32_t h,
+                  uint32_t batch, const float* params, float* grads, float* sq_err, float* A1,
+                  float* D1, float* A2, float* D2, float* slab, size_t slab_bytes, hipStream_t s,
+                  bool query_only, size_t* need) {
+  if (net->n1 == 128 && net->n2 == 64 && net->f1 == 9 && net->f2 == 5 && net->f3 == 5)
+    return run<128, 64, 9, 5, 5>(X, T, w, h, batch, params, grads, sq_err, A1, D1, A2, D2, slab,
+                                 slab_bytes, s, query_only, need);
+  return 0;
+}
+
+}  // namespace wide
+}  // namespace srcnn

@@ -1,0 +1,131 @@
+"""GPU parity of the wide-net training step (BASELINE.json configs[3]:
+n1=128, n2=64, f1=9, f2=5, f3=5; train_wide.hip) against the CPU oracle.
+
+Every intermediate the step leaves in the workspace (A1, D1, A2, D2, in the
+reference HWC layout, src/kernel/layer_uber_kernel.cl:51-56) and the
+accumulated gradients are compared with oracle/srcnn_oracle.c at
+north_star's 1e-4 normwise tolerance (hip_util.RTOL), on square, ragged
+and non-square tiles; the profile stats prove the MFMA kernels ran.
+"""
+import numpy as np
+import pytest
+
+import srcnn_oracle as orc
+from hip_util import RTOL, assert_close, make_batch, make_params
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+WIDE = (128, 64, 9, 5, 5)
+
+
+@pytest.fixture(scope="module")
+def S():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import srcnn_amd
+    srcnn_amd.set_path(0)
+    return srcnn_amd
+
+
+def D(a):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).cuda()
+
+
+def H(t):
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+def align(n):
+    return (n + 255) & ~255
+
+
+def run_step(S, w, h, batch, seed, sd=0.05, g0=None):
+    net = S.Net(*WIDE)
+    rng = np.random.default_rng(seed)
+    X, T = make_batch(rng, batch, w, h)
+    params = make_params(rng, WIDE, sd=sd)
+    P = params.size
+    if g0 is None:
+        g0 = np.zeros(P, np.float32)
+    nbytes = S.train_workspace_bytes(net, w, h, batch)
+    ws = torch.zeros(nbytes // 4 + 64, dtype=torch.float32, device="cuda")
+    g = D(g0)
+    err = torch.zeros(1, dtype=torch.float32, device="cuda")
+    S.profile_reset()
+    S.profile_enable(True)
+    S.train_fwd_bwd(net, D(X), D(T), w, h, batch, D(params), g, err, ws, nbytes)
+    torch.cuda.synchronize()
+    S.profile_enable(False)
+    stats = S.profile_stats()
+    return X, T, params, g0, H(g), float(H(err)[0]), H(ws), stats
+
+
+def split_ws(ws, w, h, batch):
+    n1, n2, f1, f2, f3 = WIDE
+    w1, h1 = w - f1 + 1, h - f1 + 1
+    w2, h2 = w1 - f2 + 1, h1 - f2 + 1
+    s1, s2 = w1 * h1 * n1 * batch, w2 * h2 * n2 * batch
+    o = 0
+    out = {}
+    for name, n in (("A1", s1), ("D1", s1), ("A2", s2), ("D2", s2)):
+        out[name] = ws[o // 4:o // 4 + n]
+        o += align(4 * n)
+    return out
+
+
+@pytest.mark.parametrize("w,h,batch", [(33, 33, 1), (33, 33, 6), (29, 29, 3), (33, 27, 2),
+                                       (25, 31, 3)])
+def test_wide_step_stages_vs_oracle(S, w, h, batch):
+    X, T, params, g0, got, err, ws, stats = run_step(S, w, h, batch, seed=7 + w + h + batch)
+    assert "wide_l2_fwd" in stats and "wide_grad2" in stats, stats.keys()
+    ref_g, acts = orc.train_fwd_bwd(WIDE, X, T, w, h, batch, params, g0, want_acts=True)
+    n1, n2, f1, f2, f3 = WIDE
+    w1, h1 = w - f1 + 1, h - f1 + 1
+    w2, h2 = w1 - f2 + 1, h1 - f2 + 1
+    w3, h3 = w2 - f3 + 1, h2 - f3 + 1
+    s1, s2, s3 = w1 * h1 * n1 * batch, w2 * h2 * n2 * batch, w3 * h3 * batch
+    rA1 = acts[:s1]
+    rA2 = acts[s1:s1 + s2]
+    rD2 = acts[s1 + s2 + 2 * s3:s1 + 2 * s2 + 2 * s3]
+    rD1 = acts[s1 + 2 * s2 + 2 * s3:]
+    st = split_ws(ws, w, h, batch)
+    assert_close(st["A1"], rA1, RTOL, "A1")
+    assert_close(st["A2"], rA2, RTOL, "A2")
+    assert_close(st["D2"], rD2, RTOL, "D2")
+    assert_close(st["D1"], rD1, RTOL, "D1")
+    net = S.Net(*WIDE)
+    off = S.net_offsets(net) + [params.size]
+    for i, nm in enumerate(["W1", "B1", "W2", "B2", "W3", "B3"]):
+        assert_close(got[off[i]:off[i + 1]], ref_g[off[i]:off[i + 1]], RTOL, "grad " + nm)
+    A3 = orc.forward(WIDE, X, w, h, batch, params)
+    ref_err = orc.sq_err(T, A3, w, h, w3, h3, batch)
+    assert err == pytest.approx(ref_err, rel=1e-4)
+
+
+def test_wide_step_accumulates_and_is_deterministic(S):
+    w = h = 33
+    batch = 300
+    rng = np.random.default_rng(3)
+    g0 = (1e-3 * rng.standard_normal(orc.param_count(*WIDE))).astype(np.float32)
+    X, T, params, _, got, _, _, _ = run_step(S, w, h, batch, seed=11, g0=g0)
+    ref_g, _ = orc.train_fwd_bwd(WIDE, X, T, w, h, batch, params, g0)
+    assert_close(got, ref_g, RTOL, "wide gradients (accumulated onto g0)")
+    _, _, _, _, got2, _, _, _ = run_step(S, w, h, batch, seed=11, g0=g0)
+    np.testing.assert_array_equal(got2, got)
+
+
+def test_wide_fast_matches_generic_path(S):
+    w = h = 33
+    batch = 64
+    fast = run_step(S, w, h, batch, seed=5)
+    S.set_path(1)
+    try:
+        gen = run_step(S, w, h, batch, seed=5)
+    finally:
+        S.set_path(0)
+    assert "wide_l2_fwd" not in gen[7]
+    assert_close(fast[4], gen[4], RTOL, "fast vs generic gradients")
+    assert fast[5] == pytest.approx(gen[5], rel=1e-4)
