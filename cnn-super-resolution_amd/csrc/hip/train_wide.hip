@@ -13,12 +13,13 @@
 //   conv_mfma    L2 forward (+bias, ReLU) and delta1 = relu'(A1) * full-conv
 //                (delta2, W2^T): input channel chunks staged HBM -> LDS by
 //                LDS-DMA (double-buffered, 80-B pixel rows: conflict-free
-//                ds_read_b128), accumulators for the whole sample in registers
+//                ds_read_b128), accumulators for the whole sample in registers;
+//                the delta1 variant feeds its masked tiles straight into
+//                gW1 / gB1 (ones row) MFMAs, so delta1 never reaches HBM
 //   wl3          L3 (Q trick) + last delta (reference relu' quirk) + squared
 //                error + delta2 (MFMA over taps) + gW3 / gB3 (MFMA over pixels)
 //   wgrad2       gW2 / gB2: 16x16x4 MFMA, K = pixels, per row band of a sample
 //                (A1 rows + delta2 rows in LDS), per-block slabs
-//   wgrad1       gW1 / gB1: K = pixels, a ones row gives gB1
 //   slab_reduce  fixed-order sum of the slabs into the gradient buffer
 //
 // Deterministic: static work assignment, fixed summation order, no atomics.
@@ -184,16 +185,29 @@ struct CGeom {
   int img_w, img_h;       // staged image = input + 2 pad
   int out_w, out_h, npx;  // output
   int batch;
+  int xw, xh;             // delta1 + gW1: the X tile (layer-1 input)
 };
 
-template <int CIN, int COUT, int F, int MT, bool DELTA>
+constexpr int kXBuf = kXTile + 64;  // X tile buffer of the fused gW1 epilogue
+
+// F1 > 0 (delta1 only): gW1 / gB1 fused into the epilogue.  The masked delta1
+// tile in the accumulators is directly the B operand of gW1 += Xwin^T delta1
+// (register s of half h is pixel crow(s, h), mfma.hpp), so delta1 never
+// leaves the CU; A = X windows (81 taps + a ones row for gB1, 3 x 32 rows)
+// from a per-item X tile DMA'd into LDS.  One gW1 slab per pair of blocks
+// (block parity = the 64-channel part, fixed because the grid is even).
+template <int CIN, int COUT, int F, int MT, bool DELTA, int F1>
 __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restrict__ in,
                                                           const float* __restrict__ Wimg,
                                                           const float* __restrict__ bias,
                                                           const float* __restrict__ ycur,
-                                                          float* __restrict__ out, CGeom g) {
+                                                          float* __restrict__ out,
+                                                          const float* __restrict__ X,
+                                                          float* __restrict__ slab1, CGeom g) {
   constexpr int NCH = CIN / kCC, FF = F * F, KSC = FF * (kCC / 8), KS = NCH * KSC;
   constexpr int NP = COUT / 64;
+  constexpr bool G1 = DELTA && F1 > 0;
+  constexpr int NT1 = F1 * F1, TT = G1 ? (NT1 + 1 + 31) / 32 : 1;
   static_assert(CIN % kCC == 0 && COUT % 64 == 0 && kCC == 16, "shape");
   extern __shared__ float smem[];
   const int lane = lane_id(), wave = wave_id(), j = lane & 31, h = lane >> 5;
@@ -201,6 +215,31 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restri
   const int img_px = g.img_w * g.img_h, slots = img_px * 5, kdma = (slots + 63) / 64;
   const int buf_floats = img_px * kPS + kImgSlack;
   const int nitems = g.batch * NP;
+  float* const xsm = smem + 2 * buf_floats;  // G1: 2 X tile buffers (item parity)
+  int toffx[TT];
+  float fill[TT];
+  bool valid[TT];
+  f32x16 gacc[TT];
+#pragma unroll
+  for (int tt = 0; tt < TT; tt++) {
+    const int tap = 32 * tt + j, tc = min(tap, NT1 - 1);
+    valid[tt] = tap < NT1;
+    fill[tt] = tap == NT1 ? 1.0f : 0.0f;
+    toffx[tt] = G1 ? (tc / F1) * kXS + tc % F1 : 0;
+    gacc[tt] = zero16();
+  }
+  // X tile of item it -> xsm[parity] by 4-byte LDS-DMA (stride kXS, zero fill)
+  auto xdma = [&](int it, int par) {
+    const int s = it / NP;
+    float* dst = xsm + par * kXBuf;
+    for (int k = wave; k * 64 < kXTile; k += 4) {
+      const int f = k * 64 + lane, row = f / kXS, col = f - row * kXS;
+      const bool ok = row < g.xh && col < g.xw;
+      __builtin_amdgcn_global_load_lds(
+          (const void*)(ok ? X + (size_t)s * g.xw * g.xh + row * g.xw + col : g_zero_src),
+          (lds_void*)(dst + k * 64), 4, 0, 0);
+    }
+  };
   int abase[MT];
 #pragma unroll
   for (int m = 0; m < MT; m++) {
@@ -225,9 +264,10 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restri
     for (int k = wave; k < kdma; k += 4) dma(blockIdx.x, 0, buf0, k);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  int bsel = 0;
-  for (int it = blockIdx.x; it < nitems; it += gridDim.x) {
+  int bsel = 0, ipar = 0;
+  for (int it = blockIdx.x; it < nitems; it += gridDim.x, ipar ^= 1) {
     const int s = it / NP, part = it - s * NP;
+    if constexpr (G1) xdma(it, ipar);  // lands before the first chunk barrier
     const float4* wp = reinterpret_cast<const float4*>(Wimg) + (size_t)(part * 2 + nt) * KS * 64 + lane;
     f32x16 acc[MT];
 #pragma unroll
@@ -292,26 +332,96 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restri
       bsel ^= 1;
     }
     const int n = part * 64 + nt * 32 + j;
-    const float bn = DELTA ? 0.0f : bias[n];
-    // one 32-pixel tile at a time; the lane index is made opaque per tile so
-    // the compiler cannot hoist all 16*MT store addresses out of the item loop
     const size_t obase = (size_t)s * g.npx * COUT + n;
-#pragma unroll
-    for (int m = 0; m < MT; m++) {
-      int hl = h;
-      asm volatile("" : "+v"(hl));
-      const int p0 = 32 * (mg * MT + m) + 4 * hl;
+    if constexpr (G1) {
+      // delta1 = relu'(A1) * acc (mask loads one tile ahead), then
+      // gW1 += Xwin^T delta1 on the matrix core
+      const float* xs = xsm + ipar * kXBuf;
+      float mk[16], mkn[16];
 #pragma unroll
       for (int r = 0; r < 16; r++) {
-        const int pix = p0 + crow(r, 0);
-        if (pix < g.npx) {
-          const size_t idx = obase + (size_t)pix * COUT;
-          if (DELTA)
-            out[idx] = ycur[idx] > 0.0f ? acc[m][r] : 0.0f;
-          else
-            out[idx] = fmaxf(acc[m][r] + bn, 0.0f);
+        const int pix = min(32 * mg * MT + crow(r, h), g.npx - 1);
+        mk[r] = ycur[obase + (size_t)pix * COUT];
+      }
+#pragma unroll
+      for (int m = 0; m < MT; m++) {
+        int hl = h;
+        asm volatile("" : "+v"(hl));
+        const int p0 = 32 * (mg * MT + m) + 4 * hl;
+        if (m + 1 < MT) {
+#pragma unroll
+          for (int r = 0; r < 16; r++) {
+            const int pix = min(p0 + 32 + crow(r, 0), g.npx - 1);
+            mkn[r] = ycur[obase + (size_t)pix * COUT];
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+          const int pix = p0 + crow(r, 0);
+          acc[m][r] = (pix < g.npx && mk[r] > 0.0f) ? acc[m][r] : 0.0f;
+        }
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+          const int pix = min(p0 + crow(r, 0), g.npx - 1), py = pix / g.out_w;
+          const int xb = py * kXS + pix - py * g.out_w;
+#pragma unroll
+          for (int tt = 0; tt < TT; tt++) {
+            const float av = xs[xb + toffx[tt]];
+            gacc[tt] = mma(valid[tt] ? av : fill[tt], acc[m][r], gacc[tt]);
+          }
+        }
+        if (m + 1 < MT) {
+#pragma unroll
+          for (int r = 0; r < 16; r++) mk[r] = mkn[r];
         }
       }
+    } else {
+      const float bn = DELTA ? 0.0f : bias[n];
+      // one 32-pixel tile at a time; the lane index is made opaque per tile so
+      // the compiler cannot hoist all 16*MT store addresses out of the item loop
+#pragma unroll
+      for (int m = 0; m < MT; m++) {
+        int hl = h;
+        asm volatile("" : "+v"(hl));
+        const int p0 = 32 * (mg * MT + m) + 4 * hl;
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+          const int pix = p0 + crow(r, 0);
+          if (pix < g.npx) {
+            const size_t idx = obase + (size_t)pix * COUT;
+            if (DELTA)
+              out[idx] = ycur[idx] > 0.0f ? acc[m][r] : 0.0f;
+            else
+              out[idx] = fmaxf(acc[m][r] + bn, 0.0f);
+          }
+        }
+      }
+    }
+  }
+  if constexpr (G1) {
+    // gW1 slab of this block pair: waves mg = 1 park their partials in LDS,
+    // waves mg = 0 add them (fixed order) and store rows tap < NT1 (+ gB1 row)
+    constexpr int P1 = NT1 * COUT + COUT;
+    __syncthreads();
+    float* red = smem;
+    if (mg == 1) {
+#pragma unroll
+      for (int tt = 0; tt < TT; tt++)
+#pragma unroll
+        for (int r = 0; r < 16; r++) red[((nt * TT + tt) * 16 + r) * 64 + lane] = gacc[tt][r];
+    }
+    __syncthreads();
+    if (mg == 0) {
+      const int ch = (blockIdx.x % NP) * 64 + 32 * nt + j;
+      float* o1 = slab1 + (size_t)(blockIdx.x / NP) * P1;
+#pragma unroll
+      for (int tt = 0; tt < TT; tt++)
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+          const int tap = 32 * tt + crow(r, h);
+          const float v = gacc[tt][r] + red[((nt * TT + tt) * 16 + r) * 64 + lane];
+          if (tap <= NT1) o1[tap * COUT + ch] = v;
+        }
     }
   }
 }
@@ -572,87 +682,6 @@ __global__ __launch_bounds__(512, 1) void wgrad2_kernel(const float* __restrict_
 }
 
 // ---------------------------------------------------------------------------
-// wgrad1: gW1[t][c] += sum_{s,q} X[q + off(t)] delta1[q][c]; gB1[c] += sum delta1
-// GEMM rows = 81 taps + a ones row (gB1) padded to 3 x 32, cols = 128 channels
-// as 4 tiles (column j of tile ct = channel 4j + ct: one float4 load per lane
-// feeds all four), K = pixel pairs split over the 4 waves.
-// ---------------------------------------------------------------------------
-template <int N1, int F1>
-__global__ __launch_bounds__(256) void wgrad1_kernel(const float* __restrict__ X,
-                                                     const float* __restrict__ D1,
-                                                     float* __restrict__ slab1, WGeom g) {
-  static_assert(N1 == 128, "4 column tiles of 32 x float4");
-  constexpr int NT = F1 * F1, TT = (NT + 1 + 31) / 32;
-  constexpr int P1 = NT * N1 + N1;
-  __shared__ float xs[kXTile];
-  extern __shared__ float red[];  // [TT*32][N1] cross-wave reduction
-  const int lane = lane_id(), wave = wave_id(), j = lane & 31, h = lane >> 5;
-  int toffx[TT];
-  float fill[TT];
-  bool valid[TT];
-#pragma unroll
-  for (int tt = 0; tt < TT; tt++) {
-    const int tap = 32 * tt + j, tc = min(tap, NT - 1);
-    valid[tt] = tap < NT;
-    fill[tt] = tap == NT ? 1.0f : 0.0f;
-    toffx[tt] = (tc / F1) * kXS + tc % F1;
-  }
-  f32x16 acc[TT][4];
-#pragma unroll
-  for (int tt = 0; tt < TT; tt++)
-#pragma unroll
-    for (int ct = 0; ct < 4; ct++) acc[tt][ct] = zero16();
-  for (int i = threadIdx.x; i < kXTile; i += 256) xs[i] = 0.0f;
-  const int npx = g.w1 * g.h1;
-  for (int s = blockIdx.x; s < g.batch; s += gridDim.x) {
-    __syncthreads();
-    const float* xsrc = X + (size_t)s * g.w * g.h;
-    for (int i = threadIdx.x; i < g.w * g.h; i += 256) {
-      const int y = i / g.w;
-      xs[y * kXS + i - y * g.w] = xsrc[i];
-    }
-    __syncthreads();
-    const float4* dsrc = reinterpret_cast<const float4*>(D1 + (size_t)s * npx * N1) + j;
-    for (int kp = wave; 2 * kp < npx; kp += 4) {
-      const int pk = 2 * kp + h;
-      const bool pok = pk < npx;
-      const int p = pok ? pk : npx - 1, py = p / g.w1, px = p - py * g.w1;
-      float4 b = dsrc[(size_t)p * (N1 / 4)];
-      if (!pok) b = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-      const int xb = py * kXS + px;
-#pragma unroll
-      for (int tt = 0; tt < TT; tt++) {
-        const float av = xs[xb + toffx[tt]];
-        const float a = valid[tt] ? av : fill[tt];
-        acc[tt][0] = mma(a, b.x, acc[tt][0]);
-        acc[tt][1] = mma(a, b.y, acc[tt][1]);
-        acc[tt][2] = mma(a, b.z, acc[tt][2]);
-        acc[tt][3] = mma(a, b.w, acc[tt][3]);
-      }
-    }
-  }
-  // fixed-order cross-wave sum: wave 0 stores, waves 1..3 add in turn
-  for (int w = 0; w < 4; w++) {
-    __syncthreads();
-    if (wave == w) {
-#pragma unroll
-      for (int tt = 0; tt < TT; tt++)
-#pragma unroll
-        for (int ct = 0; ct < 4; ct++)
-#pragma unroll
-          for (int r = 0; r < 16; r++) {
-            const int row = 32 * tt + crow(r, h), col = 4 * j + ct;
-            float* d = red + row * N1 + col;
-            *d = w == 0 ? acc[tt][ct][r] : *d + acc[tt][ct][r];
-          }
-    }
-  }
-  __syncthreads();
-  float* out = slab1 + (size_t)blockIdx.x * P1;
-  for (int e = threadIdx.x; e < (NT + 1) * N1; e += 256) out[e] = red[e];
-}
-
-// ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
 template <int N1, int N2, int F1, int F2, int F3>
@@ -695,8 +724,9 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   if (g.w > kXS || g.h > kXS || g.w3 <= 0 || g.h3 <= 0) return 0;
   const int npx1 = g.w1 * g.h1, npx2 = g.w2 * g.h2;
   // L2 forward / delta1 geometry limits (register tiles, LDS images)
-  CGeom cf{g.w1, g.h1, 0, g.w1, g.h1, g.w2, g.h2, npx2, g.batch};
-  CGeom cd{g.w2, g.h2, F2 - 1, g.w2 + 2 * (F2 - 1), g.h2 + 2 * (F2 - 1), g.w1, g.h1, npx1, g.batch};
+  CGeom cf{g.w1, g.h1, 0, g.w1, g.h1, g.w2, g.h2, npx2, g.batch, 0, 0};
+  CGeom cd{g.w2, g.h2, F2 - 1, g.w2 + 2 * (F2 - 1), g.h2 + 2 * (F2 - 1), g.w1, g.h1, npx1, g.batch,
+           g.w, g.h};
   if ((npx2 + 31) / 32 > 2 * NetT::MT2 || (npx1 + 31) / 32 > 2 * NetT::MT4) return 0;
   if (cf.img_w * cf.img_h > kImgMax || cd.img_w * cd.img_h > kImgMax) return 0;
   // wgrad2 bands
@@ -714,7 +744,9 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   const int qfloats = std::max(npx2 * F3 * F3, 2 * 16 * 64 * 4);
   const size_t lds3 = (size_t)(qfloats + (g.w3 + 2 * (F3 - 1)) * (g.h3 + 2 * (F3 - 1))) * 4;
   if (lds3 > 64 * 1024) return 0;
-  const int G1 = (int)std::min<uint32_t>(batch, 512);
+  constexpr int NPD = N1 / 64;  // delta1 items per sample (64-channel parts)
+  const int GD = std::min(g.batch * NPD, 256);  // a multiple of NPD: block parity = part
+  const int G1 = GD / NPD;                      // gW1 slabs: one per block pair
   const int G3 = (int)std::min<uint32_t>(batch, 512);
   const int GC = 256;
   const int G2 = g2.groups * (N1 / 32);
@@ -757,10 +789,11 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   {
     SRCNN_PROFILE("wide_l2_fwd", s);
     const size_t lds = 2 * ((size_t)cf.img_w * cf.img_h * kPS + kImgSlack) * sizeof(float);
-    if (int rc = set_lds(conv_mfma_kernel<N1, N2, F2, NetT::MT2, false>, lds)) return rc;
+    if (int rc = set_lds(conv_mfma_kernel<N1, N2, F2, NetT::MT2, false, 0>, lds)) return rc;
     const int items = g.batch * (N2 / 64);
-    hipLaunchKernelGGL((conv_mfma_kernel<N1, N2, F2, NetT::MT2, false>), dim3(std::min(items, GC)), dim3(256), lds, s, A1, Wf, B2,
-                       (const float*)nullptr, A2, cf);
+    hipLaunchKernelGGL((conv_mfma_kernel<N1, N2, F2, NetT::MT2, false, 0>), dim3(std::min(items, GC)),
+                       dim3(256), lds, s, A1, Wf, B2, (const float*)nullptr, A2, (const float*)nullptr,
+                       (float*)nullptr, cf);
     SRCNN_LAUNCH_TRY();
   }
   {
@@ -771,12 +804,12 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
     SRCNN_LAUNCH_TRY();
   }
   {
-    SRCNN_PROFILE("wide_delta1", s);
-    const size_t lds = 2 * ((size_t)cd.img_w * cd.img_h * kPS + kImgSlack) * sizeof(float);
-    if (int rc = set_lds(conv_mfma_kernel<N2, N1, F2, NetT::MT4, true>, lds)) return rc;
-    const int items = g.batch * (N1 / 64);
-    hipLaunchKernelGGL((conv_mfma_kernel<N2, N1, F2, NetT::MT4, true>), dim3(std::min(items, GC)), dim3(256), lds, s, D2, Wd,
-                       (const float*)nullptr, A1, D1, cd);
+    SRCNN_PROFILE("wide_delta1_grad1", s);
+    const size_t lds =
+        (2 * ((size_t)cd.img_w * cd.img_h * kPS + kImgSlack) + 2 * kXBuf) * sizeof(float);
+    if (int rc = set_lds(conv_mfma_kernel<N2, N1, F2, NetT::MT4, true, F1>, lds)) return rc;
+    hipLaunchKernelGGL((conv_mfma_kernel<N2, N1, F2, NetT::MT4, true, F1>), dim3(GD), dim3(256),
+                       lds, s, D2, Wd, (const float*)nullptr, A1, (float*)nullptr, X, slab1, cd);
     SRCNN_LAUNCH_TRY();
   }
   {
@@ -784,13 +817,6 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
     const size_t lds = 2 * (size_t)kGBuf * sizeof(float);
     if (int rc = set_lds(wgrad2_kernel<N1, N2, F2>, lds)) return rc;
     hipLaunchKernelGGL((wgrad2_kernel<N1, N2, F2>), dim3(G2), dim3(512), lds, s, A1, D2, slab2, g2);
-    SRCNN_LAUNCH_TRY();
-  }
-  {
-    SRCNN_PROFILE("wide_grad1", s);
-    const size_t lds = (size_t)((F1 * F1 + 1 + 31) / 32 * 32) * N1 * sizeof(float);
-    if (int rc = set_lds(wgrad1_kernel<N1, F1>, lds)) return rc;
-    hipLaunchKernelGGL((wgrad1_kernel<N1, F1>), dim3(G1), dim3(256), lds, s, X, D1, slab1, g);
     SRCNN_LAUNCH_TRY();
   }
   {

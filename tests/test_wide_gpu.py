@@ -1,8 +1,9 @@
 """GPU parity of the wide-net training step (BASELINE.json configs[3]:
 n1=128, n2=64, f1=9, f2=5, f3=5; train_wide.hip) against the CPU oracle.
 
-Every intermediate the step leaves in the workspace (A1, D1, A2, D2, in the
-reference HWC layout, src/kernel/layer_uber_kernel.cl:51-56) and the
+Every intermediate the step leaves in the workspace (A1, A2, D2, in the
+reference HWC layout, src/kernel/layer_uber_kernel.cl:51-56; delta1 stays
+inside the delta1+gW1 kernel and is checked through gW1 / gB1) and the
 accumulated gradients are compared with oracle/srcnn_oracle.c at
 north_star's 1e-4 normwise tolerance (hip_util.RTOL), on square, ragged
 and non-square tiles; the profile stats prove the MFMA kernels ran.
@@ -90,12 +91,10 @@ def test_wide_step_stages_vs_oracle(S, w, h, batch):
     rA1 = acts[:s1]
     rA2 = acts[s1:s1 + s2]
     rD2 = acts[s1 + s2 + 2 * s3:s1 + 2 * s2 + 2 * s3]
-    rD1 = acts[s1 + 2 * s2 + 2 * s3:]
     st = split_ws(ws, w, h, batch)
     assert_close(st["A1"], rA1, RTOL, "A1")
     assert_close(st["A2"], rA2, RTOL, "A2")
     assert_close(st["D2"], rD2, RTOL, "D2")
-    assert_close(st["D1"], rD1, RTOL, "D1")
     net = S.Net(*WIDE)
     off = S.net_offsets(net) + [params.size]
     for i, nm in enumerate(["W1", "B1", "W2", "B2", "W3", "B3"]):
