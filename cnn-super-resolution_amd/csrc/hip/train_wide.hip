@@ -27,6 +27,9 @@
 #include "mfma.hpp"
 #include "ops.hpp"
 
+// M0 is written only by the LDS-DMA asm below (nothing else in this file uses it)
+#pragma clang diagnostic ignored "-Winline-asm"
+
 namespace srcnn {
 namespace wide {
 
@@ -45,8 +48,27 @@ typedef __attribute__((address_space(3))) void lds_void;
 // 16-B zero source for the LDS-DMA of padding / out-of-image slots
 __device__ float g_zero_src[64] = {0.0f};
 
+// LDS-DMA (global_load_lds, 16 or 4 B per lane into M0 + 16 / 4 * lane) as
+// inline asm: issued through the builtin, the compiler cannot tell the
+// in-flight DMA into the NEXT buffer from reads of the current one and puts
+// an s_waitcnt vmcnt(0) before every later LDS read, which drains the whole
+// prefetch each k-step.  Hidden from it, its own vmcnt waits only under-count
+// (stay safe); every consumer reaches the data through an explicit
+// s_waitcnt vmcnt(0) + barrier.
+__device__ __forceinline__ uint32_t lds_addr(const float* p) {
+  return (uint32_t)reinterpret_cast<uintptr_t>((lds_void*)p);
+}
 __device__ __forceinline__ void dma16(const float* src, float* lds_dst) {
-  __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)lds_dst, 16, 0, 0);
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
+               :
+               : "s"(__builtin_amdgcn_readfirstlane(lds_addr(lds_dst))), "v"(src)
+               : "m0");
+}
+__device__ __forceinline__ void dma4(const float* src, float* lds_dst) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dword %1, off"
+               :
+               : "s"(__builtin_amdgcn_readfirstlane(lds_addr(lds_dst))), "v"(src)
+               : "m0");
 }
 
 struct WGeom {
@@ -235,9 +257,7 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restri
     for (int k = wave; k * 64 < kXTile; k += 4) {
       const int f = k * 64 + lane, row = f / kXS, col = f - row * kXS;
       const bool ok = row < g.xh && col < g.xw;
-      __builtin_amdgcn_global_load_lds(
-          (const void*)(ok ? X + (size_t)s * g.xw * g.xh + row * g.xw + col : g_zero_src),
-          (lds_void*)(dst + k * 64), 4, 0, 0);
+      dma4(ok ? X + (size_t)s * g.xw * g.xh + row * g.xw + col : g_zero_src, dst + k * 64);
     }
   };
   int abase[MT];
@@ -272,13 +292,15 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restri
     f32x16 acc[MT];
 #pragma unroll
     for (int m = 0; m < MT; m++) acc[m] = zero16();
-    // B operands of taps t, t+1, t+2 (2 k-steps each) in flight
-    float4 b0[2], b1[2], b2[2];
+    // B operands: a ring of 5 taps (2 k-steps each), tap t in slot t % F;
+    // the loads run 4 taps ahead and land straight in their slot (the dx
+    // loop is unrolled, so no register moves wait on a pending load)
+    static_assert(F == 5, "B ring sized for 5x5 taps");
+    float4 bq[F][2];
 #pragma unroll
-    for (int q = 0; q < 2; q++) {
-      b0[q] = wp[(size_t)q * 64];
-      b1[q] = wp[(size_t)(2 + q) * 64];
-    }
+    for (int d = 0; d < F - 1; d++)
+#pragma unroll
+      for (int q = 0; q < 2; q++) bq[d][q] = wp[(size_t)(2 * d + q) * 64];
     for (int c = 0; c < NCH; c++) {
       const float* cur = bsel ? buf1 : buf0;
       float* nxt = bsel ? buf0 : buf1;
@@ -292,39 +314,45 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restri
 #pragma unroll
       for (int m = 0; m < MT; m++) a[m] = *reinterpret_cast<const float4*>(cur + abase[m]);
 #pragma unroll 1
-      for (int t = 0; t < FF; t++) {
-        const int toff = ((t / F) * g.img_w + (t % F)) * kPS;
-        const int tn = t + 1 < FF ? t + 1 : t;
-        const int toffn = ((tn / F) * g.img_w + (tn % F)) * kPS;
-        const int ksb = c * KSC + 2 * (t + 2);  // first k-step of tap t + 2
+      for (int dy = 0; dy < F; dy++) {
 #pragma unroll
-        for (int q = 0; q < 2; q++) b2[q] = wp[(size_t)min(ksb + q, KS - 1) * 64];
-        // this tap's share of the next chunk's DMA (issued after the B loads)
+        for (int dx = 0; dx < F; dx++) {
+          const int t = dy * F + dx;
+          const int toff = (dy * g.img_w + dx) * kPS;
+          const int tn = dx + 1 < F ? t + 1 : (dy + 1 < F ? t + 1 : t);
+          const int toffn = ((tn / F) * g.img_w + (tn % F)) * kPS;
+          // B of tap t + 4 into the slot tap t - 1 used
+          const int ksb = c * KSC + 2 * (t + F - 1);
 #pragma unroll
-        for (int q = 0; q < 2; q++) {
-          const int k = wave + 4 * (2 * t + q);
-          if (stage && k < kdma) dma(nit, nc, nxt, k);
-        }
-        // k-step (t, 0): prefetch (t, 1)
+          for (int q = 0; q < 2; q++)
+            bq[(dx + F - 1) % F][q] = wp[(size_t)min(ksb + q, KS - 1) * 64];
+          // this tap's share of the next chunk's DMA (issued after the B loads)
 #pragma unroll
-        for (int m = 0; m < MT; m++)
-          an[m] = *reinterpret_cast<const float4*>(cur + abase[m] + toff + 8);
+          for (int q = 0; q < 2; q++) {
+            const int k = wave + 4 * (2 * t + q);
+            if (stage && k < kdma) dma(nit, nc, nxt, k);
+          }
+          // k-step (t, 0) while (t, 1) loads; k-step (t, 1) while (t + 1, 0)
+          // loads.  sched_barriers pin the order: left alone, the scheduler
+          // sinks the prefetch reads below the MFMAs and exposes LDS latency.
 #pragma unroll
-        for (int jj = 0; jj < 4; jj++)
+          for (int m = 0; m < MT; m++)
+            an[m] = *reinterpret_cast<const float4*>(cur + abase[m] + toff + 8);
+          __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-          for (int m = 0; m < MT; m++) acc[m] = mma(a[m][jj], b0[0][jj], acc[m]);
-        // k-step (t, 1): prefetch (t + 1, 0)
+          for (int jj = 0; jj < 4; jj++)
 #pragma unroll
-        for (int m = 0; m < MT; m++)
-          a[m] = *reinterpret_cast<const float4*>(cur + abase[m] + toffn);
+            for (int m = 0; m < MT; m++) acc[m] = mma(a[m][jj], bq[dx][0][jj], acc[m]);
+          __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int jj = 0; jj < 4; jj++)
+          for (int m = 0; m < MT; m++)
+            a[m] = *reinterpret_cast<const float4*>(cur + abase[m] + toffn);
+          __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-          for (int m = 0; m < MT; m++) acc[m] = mma(an[m][jj], b0[1][jj], acc[m]);
+          for (int jj = 0; jj < 4; jj++)
 #pragma unroll
-        for (int q = 0; q < 2; q++) {
-          b0[q] = b1[q];
-          b1[q] = b2[q];
+            for (int m = 0; m < MT; m++) acc[m] = mma(an[m][jj], bq[dx][1][jj], acc[m]);
+          __builtin_amdgcn_sched_barrier(0);
         }
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

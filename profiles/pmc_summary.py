@@ -22,6 +22,12 @@ SHORT = [
     (r"l3_delta_kernel", "l3_delta_fused"),
     (r"d1_grad12_kernel", "delta1_grad12_fused"),
     (r"slab_reduce_kernel", "slab_reduce"),
+    (r"wide::prepack_w2_kernel", "wide_prepack_w2"),
+    (r"wide::wl1_fwd_kernel", "wide_l1_fwd"),
+    (r"wide::conv_mfma_kernel<128, 64", "wide_l2_fwd"),
+    (r"wide::conv_mfma_kernel<64, 128", "wide_delta1_grad1"),
+    (r"wide::wl3_kernel", "wide_l3_delta"),
+    (r"wide::wgrad2_kernel", "wide_grad2"),
     (r"sgd_update_kernel", "sgd_update"),
     (r"update_all_kernel", "update_all"),
     (r"fill_kernel", "fill"),
