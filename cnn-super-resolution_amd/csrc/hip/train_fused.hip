@@ -37,6 +37,9 @@ using mfma::mma;
 using mfma::zero16;
 
 constexpr int kXsMax = 1536;  // input sample / region tile (floats) staged in LDS (<= 39x39)
+constexpr int kL12S = 40;                     // l12_fwd X tile row stride (w, h <= 40)
+constexpr int kL12Tile = kL12S * (kL12S + 1);  // + a zero row read by the padded tap
+constexpr int kL12Regs = (kL12S * kL12S + 255) / 256;
 
 struct Geom {
   int W, H;      // input sample
@@ -54,8 +57,9 @@ __global__ __launch_bounds__(256, 2) void l12_fwd_kernel(
     float* __restrict__ A2, Geom g) {
   constexpr int K1 = F1 * F1, KS1 = (K1 + 1) / 2, NT1 = N1 / 32;
   constexpr int NT2 = (N2 + 31) / 32, KS2 = N1 / 2;
-  constexpr int TS = N1 + 1;  // padded row of the per-wave A1 transpose
-  __shared__ float xs[kXsMax];
+  constexpr int TS = N1 + 4;  // row of the per-wave A1 transpose (16-B aligned, 272-B rows:
+                              // conflict-free ds_read_b128 / ds_write_b32)
+  __shared__ float xs[kL12Tile];  // X tile at the fixed row stride kL12S (+ zero rows)
   __shared__ float ts[4][32][TS];
 
   const int lane = mfma::lane_id(), wave = mfma::wave_id();
@@ -75,7 +79,8 @@ __global__ __launch_bounds__(256, 2) void l12_fwd_kernel(
   float b1v[NT1];
 #pragma unroll
   for (int t = 0; t < NT1; t++) b1v[t] = B1[32 * t + li];
-  // B operands of L2: W2[c = 2s + h][n = 32u + li]
+  // B operands of L2: W2[c = KS2*h + s][n = 32u + li] (half h contracts the
+  // contiguous channels [KS2*h, KS2*h + KS2): its A operands are 16-B reads)
   float w2f[KS2][NT2];
   float b2v[NT2];
 #pragma unroll
@@ -83,105 +88,117 @@ __global__ __launch_bounds__(256, 2) void l12_fwd_kernel(
 #pragma unroll
     for (int u = 0; u < NT2; u++) {
       const int n = 32 * u + li;
-      w2f[s][u] = n < N2 ? W2[(2 * s + h) * N2 + n] : 0.0f;
+      w2f[s][u] = n < N2 ? W2[(KS2 * h + s) * N2 + n] : 0.0f;
     }
 #pragma unroll
   for (int u = 0; u < NT2; u++) b2v[u] = (32 * u + li) < N2 ? B2[32 * u + li] : 0.0f;
 
+  // The next sample's X tile is register-staged during the current sample
+  // (its loads retire under the MFMAs instead of stalling both barriers);
+  // the LDS copy uses a fixed row stride so every L1 A operand is a per-half
+  // base + immediate (tap 2s+1 sits 1 or kL12S - F1 + 1 floats past tap 2s).
+  for (int i = threadIdx.x; i < kL12Tile; i += blockDim.x) xs[i] = 0.0f;
+  const int xn = g.W * g.H;
+  float xr[kL12Regs];
+  auto xload = [&](int smp) {
+    const float* src = X + (size_t)smp * xn;
+#pragma unroll
+    for (int k = 0; k < kL12Regs; k++) {
+      const int i = threadIdx.x + 256 * k;
+      xr[k] = i < xn ? src[i] : 0.0f;
+    }
+  };
+  if ((int)blockIdx.x < g.batch) xload(blockIdx.x);
   for (int sample = blockIdx.x; sample < g.batch; sample += gridDim.x) {
     __syncthreads();  // previous sample's readers are done with xs
-    const float* xsrc = X + (size_t)sample * g.W * g.H;
-    for (int i = threadIdx.x; i < g.W * g.H; i += blockDim.x) xs[i] = xsrc[i];
+#pragma unroll
+    for (int k = 0; k < kL12Regs; k++) {
+      const int i = threadIdx.x + 256 * k;
+      if (i < xn) {
+        const int y = i / g.W;
+        xs[y * kL12S + i - y * g.W] = xr[k];
+      }
+    }
     __syncthreads();
+    if (sample + (int)gridDim.x < g.batch) xload(sample + gridDim.x);
 
     for (int c = wave; c < nch; c += 4) {
       // this lane's own pixel (A-operand row li)
       const int pc = min(c * 32 + li, npx - 1);
       const int iy = pc / g.ow, ix = pc - iy * g.ow;
-      const int xb = iy * g.W + ix;
+      const int xbA = iy * kL12S + ix + h, xbB = xbA + h * (kL12S - F1);
 
       f32x16 acc1[NT1];
 #pragma unroll
       for (int t = 0; t < NT1; t++) acc1[t] = zero16();
 #pragma unroll
       for (int s = 0; s < KS1; s++) {
-        const int k0 = 2 * s, k1 = 2 * s + 1;
-        const int o0 = (k0 / F1) * g.W + (k0 % F1);
-        const int o1 = k1 < K1 ? (k1 / F1) * g.W + (k1 % F1) : 0;
-        const float a = xs[xb + (h ? o1 : o0)];
+        const int k0 = 2 * s;
+        const int o0 = (k0 / F1) * kL12S + (k0 % F1);
+        const float a = xs[((k0 % F1) + 1 < F1 ? xbA : xbB) + o0];
 #pragma unroll
         for (int t = 0; t < NT1; t++) acc1[t] = mma(a, w1f[s][t], acc1[t]);
       }
 
-      // epilogue L1: bias + ReLU (layer_uber_kernel.cl:88-95) in place, into
-      // the per-wave LDS transpose that feeds L2's A operand.  The A1 stores
-      // (HWC) are issued after the L2 MFMAs, so they stream out while the
-      // matrix core works.  Output row crow(r, h) of the chunk is pixel
-      // c*32 + crow(r, h): the store address is a per-lane base plus an immediate.
+      // epilogue L1: bias + ReLU (layer_uber_kernel.cl:88-95) into the
+      // per-wave LDS transpose (rows = the chunk's 32 pixels, HWC order).
+      // That image is both L2's A operand and the source of the A1 stores:
+      // the chunk's A1 rows are one contiguous run in HBM, written as
+      // 16-B-per-lane coalesced stores (N1/8 per lane instead of 16*NT1
+      // scattered dword stores), issued under the L2 MFMAs.
 #pragma unroll
       for (int r = 0; r < 16; r++)
 #pragma unroll
-        for (int t = 0; t < NT1; t++) {
-          acc1[t][r] = fmaxf(acc1[t][r] + b1v[t], 0.0f);
-          ts[wave][crow(r, h)][32 * t + li] = acc1[t][r];
-        }
+        for (int t = 0; t < NT1; t++)
+          ts[wave][crow(r, h)][32 * t + li] = fmaxf(acc1[t][r] + b1v[t], 0.0f);
       __builtin_amdgcn_wave_barrier();
+      // L2 A operands: this lane's pixel, channels [KS2*h, KS2*h + KS2)
+      float a2v[KS2];
+#pragma unroll
+      for (int q = 0; q < KS2 / 4; q++) {
+        const float4 v = *reinterpret_cast<const float4*>(&ts[wave][li][KS2 * h + 4 * q]);
+        a2v[4 * q] = v.x;
+        a2v[4 * q + 1] = v.y;
+        a2v[4 * q + 2] = v.z;
+        a2v[4 * q + 3] = v.w;
+      }
+      // A1 stores: float4 f = 64 i + lane of the chunk is pixel f / (N1/4);
+      // fire-and-forget, they drain while the L2 MFMAs below run
+      constexpr int Q1 = N1 / 4, NS1 = 32 * Q1 / 64;
+      const int p0 = c * 32;  // first pixel of the chunk
+      float* a1c = A1 + ((size_t)sample * npx + p0) * N1;
+      const bool full = p0 + 32 <= npx;  // wave-uniform
+#pragma unroll
+      for (int i = 0; i < NS1; i++) {
+        const int f = 64 * i + lane;
+        const float4 v = *reinterpret_cast<const float4*>(&ts[wave][f / Q1][4 * (f % Q1)]);
+        if (full || p0 + f / Q1 < npx)
+          *reinterpret_cast<float4*>(a1c + (size_t)(f / Q1) * N1 + 4 * (f % Q1)) = v;
+      }
       f32x16 acc2[NT2];
 #pragma unroll
       for (int u = 0; u < NT2; u++) acc2[u] = zero16();
-      const int q0 = c * 32 + 4 * h;  // pixel of register 0 of this lane half
-      float* a1row = A1 + ((size_t)sample * npx + q0) * N1 + li;
-      const bool full = c * 32 + 32 <= npx;  // wave-uniform
-      if (full) {
-        // one scheduling region: per k-step 1 LDS read, NT2 MFMAs and 2 of
-        // the 32*NT1/16 A1 stores, interleaved so the stores stream out
-        // under the MFMAs
 #pragma unroll
-        for (int s = 0; s < KS2; s++) {
-          const float a = ts[wave][li][2 * s + h];
+      for (int s = 0; s < KS2; s++)
 #pragma unroll
-          for (int u = 0; u < NT2; u++) acc2[u] = mma(a, w2f[s][u], acc2[u]);
-        }
+        for (int u = 0; u < NT2; u++) acc2[u] = mma(a2v[s], w2f[s][u], acc2[u]);
+      // epilogue L2: bias + ReLU into the same transpose (columns 0..N2-1),
+      // then the chunk's A2 rows as coalesced 16-B stores
+      __builtin_amdgcn_wave_barrier();
 #pragma unroll
-        for (int r = 0; r < 16; r++)
+      for (int r = 0; r < 16; r++)
 #pragma unroll
-          for (int t = 0; t < NT1; t++) {
-#ifndef SRCNN_L12_NO_A1STORE  // diagnostics only
-            a1row[((r & 3) + 8 * (r >> 2)) * N1 + 32 * t] = acc1[t][r];
-#endif
-          }
-        constexpr int kStoresPerStep = (16 * NT1 + KS2 - 1) / KS2;
+        for (int u = 0; u < NT2; u++)
+          if (32 * u + li < N2) ts[wave][crow(r, h)][32 * u + li] = fmaxf(acc2[u][r] + b2v[u], 0.0f);
+      __builtin_amdgcn_wave_barrier();
+      constexpr int Q2 = N2 / 4, NS2 = (32 * Q2 + 63) / 64;
+      float* a2c = A2 + ((size_t)sample * npx + p0) * N2;
 #pragma unroll
-        for (int s = 0; s < KS2; s++) {
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);              // DS read
-          __builtin_amdgcn_sched_group_barrier(0x008, NT2, 0);            // MFMA
-          __builtin_amdgcn_sched_group_barrier(0x040, kStoresPerStep, 0); // VMEM write
-        }
-      } else {
-#pragma unroll
-        for (int s = 0; s < KS2; s++) {
-          const float a = ts[wave][li][2 * s + h];
-#pragma unroll
-          for (int u = 0; u < NT2; u++) acc2[u] = mma(a, w2f[s][u], acc2[u]);
-        }
-#pragma unroll
-        for (int r = 0; r < 16; r++) {
-          const int rr = (r & 3) + 8 * (r >> 2);  // crow(r, h) - 4h
-#pragma unroll
-          for (int t = 0; t < NT1; t++)
-            if (q0 + rr < npx) a1row[rr * N1 + 32 * t] = acc1[t][r];
-        }
-      }
-      float* a2row = A2 + ((size_t)sample * npx + q0) * N2 + li;
-#pragma unroll
-      for (int r = 0; r < 16; r++) {
-        const int rr = (r & 3) + 8 * (r >> 2);
-        const bool ok = q0 + rr < npx;
-#pragma unroll
-        for (int u = 0; u < NT2; u++) {
-          const int n = 32 * u + li;
-          if (ok && n < N2) a2row[rr * N2 + 32 * u] = fmaxf(acc2[u][r] + b2v[u], 0.0f);
-        }
+      for (int i = 0; i < NS2; i++) {
+        const int f = 64 * i + lane;
+        if (f < 32 * Q2 && (full || p0 + f / Q2 < npx))
+          *reinterpret_cast<float4*>(a2c + (size_t)(f / Q2) * N2 + 4 * (f % Q2)) =
+              *reinterpret_cast<const float4*>(&ts[wave][f / Q2][4 * (f % Q2)]);
       }
       __builtin_amdgcn_wave_barrier();
     }
@@ -661,7 +678,7 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   using NetT = Net<N1, N2, F1, F3>;
   const int ow = w - F1 + 1, oh = h - F1 + 1;
   const int w3 = ow - F3 + 1, h3 = oh - F3 + 1;
-  if ((int)(w * h) > kXsMax || w3 <= 0 || h3 <= 0) return 0;
+  if ((int)(w * h) > kXsMax || (int)w > kL12S || (int)h > kL12S || w3 <= 0 || h3 <= 0) return 0;
   const size_t lds3 = l3_lds_bytes<N2, F3>(ow, oh);
   if (lds3 > 160 * 1024 || w3 * h3 > kL3MaxOut) return 0;
   const int g12 = grid_for_batch(batch, 1024);
