@@ -323,19 +323,23 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
   do {                                                                            \
     int l_ = lane; /* opaque: the address is formed here, never held */           \
     asm volatile("" : "+v"(l_));                                                  \
+    /* wave-uniform chunk bases (SGPRs) + 32-bit per-lane offsets: the DMA */     \
+    /* takes the saddr form, no 64-bit address math per instruction */           \
+    const int rmax_ = npx - 1 - (C) * 32;                                         \
+    const size_t px0_ = (size_t)(SMP) * npx + (size_t)(C) * 32;                   \
     if ((K) < A1K) {                                                              \
-      const int f_ = (K) * 256 + 4 * l_;                                          \
-      const int r_ = f_ / A1P, col_ = f_ - (f_ / A1P) * A1P;                      \
-      const int row_ = min((C) * 32 + r_, npx - 1);                               \
+      const uint32_t f_ = (K) * 256 + 4 * (uint32_t)l_;                           \
+      const uint32_t r_ = f_ / A1P, col_ = f_ - r_ * A1P;                         \
+      const uint32_t off_ = (uint32_t)min((int)r_, rmax_) * N1 + (col_ < N1 ? col_ : 0u); \
       __builtin_amdgcn_global_load_lds(                                           \
-          (const void*)(A1 + (size_t)(SMP) * npx * N1 + (row_ * N1 + (col_ < N1 ? col_ : 0))), \
+          (const void*)(A1 + px0_ * N1 + off_),                                   \
           (__attribute__((address_space(3))) void*)(a1me + (K) * 256), 16, 0, 0); \
     } else {                                                                      \
-      const int f_ = 64 * ((K) - A1K) + l_;                                       \
-      const int r_ = f_ / DS, col_ = f_ - (f_ / DS) * DS;                         \
-      const int row_ = min((C) * 32 + r_, npx - 1);                               \
+      const uint32_t f_ = 64 * ((K) - A1K) + (uint32_t)l_;                        \
+      const uint32_t r_ = f_ / DS, col_ = f_ - r_ * DS;                           \
+      const uint32_t off_ = (uint32_t)min((int)r_, rmax_) * N2 + (col_ < N2 ? col_ : 0u); \
       __builtin_amdgcn_global_load_lds(                                           \
-          (const void*)(D2 + (size_t)(SMP) * npx * N2 + row_ * N2 + (col_ < N2 ? col_ : 0)), \
+          (const void*)(D2 + px0_ * N2 + off_),                                   \
           (__attribute__((address_space(3))) void*)(d2me + 64 * ((K) - A1K)), 4, 0, 0); \
     }                                                                             \
   } while (0)
