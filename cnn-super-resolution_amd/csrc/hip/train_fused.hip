@@ -50,52 +50,50 @@ struct Geom {
 // ---------------------------------------------------------------------------
 // Kernel 1: L1 (+ L2) forward, one sample per work item
 // ---------------------------------------------------------------------------
+// Both layers run TRANSPOSED (rows = channels, cols = the chunk's 32 pixels):
+//   L1^T: A1^T[ch][p] = sum_tap W1[tap][ch] X[p + off(tap)]   A = W1 (registers),
+//         B = X gathers from LDS; the padded k-slot (tap 81) reads 1.0 against
+//         B1, so the bias rides in the GEMM
+//   L2^T: A2^T[n][p] = sum_c W2[c][n] A1^T[c][p]   B = the L1 accumulator
+//         registers as they stand (register s of half h is channel crow(s, h),
+//         mfma.hpp), A = W2 (registers); one extra MFMA adds B2
+// so L2 needs no LDS transpose at all, and each lane ends with consecutive
+// channels of ONE pixel: A1 / A2 leave as 16-B stores straight from registers.
 template <int N1, int N2, int F1>
 __global__ __launch_bounds__(256, 2) void l12_fwd_kernel(
     const float* __restrict__ X, const float* __restrict__ W1, const float* __restrict__ B1,
     const float* __restrict__ W2, const float* __restrict__ B2, float* __restrict__ A1,
     float* __restrict__ A2, Geom g) {
   constexpr int K1 = F1 * F1, KS1 = (K1 + 1) / 2, NT1 = N1 / 32;
-  constexpr int NT2 = (N2 + 31) / 32, KS2 = N1 / 2;
-  constexpr int TS = N1 + 4;  // row of the per-wave A1 transpose (16-B aligned, 272-B rows:
-                              // conflict-free ds_read_b128 / ds_write_b32)
+  static_assert(N2 <= 32 && N2 % 8 == 0 && K1 % 2 == 1 && N1 % 32 == 0,
+                "transposed l12: one 32-row L2 tile, odd tap count");
   __shared__ float xs[kL12Tile];  // X tile at the fixed row stride kL12S (+ zero rows)
-  __shared__ float ts[4][32][TS];
 
   const int lane = mfma::lane_id(), wave = mfma::wave_id();
   const int h = lane >> 5, li = lane & 31;
   const int npx = g.ow * g.oh;
   const int nch = (npx + 31) / 32;
 
-  // B operands of L1: W1[tap = 2s + h][n = 32t + li]
+  // A operands of L1^T: W1[tap = 2s + h][ch = 32t + li]; tap K1 is the bias slot
   float w1f[KS1][NT1];
 #pragma unroll
   for (int s = 0; s < KS1; s++)
 #pragma unroll
     for (int t = 0; t < NT1; t++) {
       const int tap = 2 * s + h;
-      w1f[s][t] = tap < K1 ? W1[tap * N1 + 32 * t + li] : 0.0f;
+      w1f[s][t] = tap < K1 ? W1[tap * N1 + 32 * t + li] : B1[32 * t + li];
     }
-  float b1v[NT1];
+  // A operands of L2^T: W2[c = 32t + crow(s, h)][n = li]; bias MFMA: B2[li] (half 0)
+  float w2f[NT1][16];
 #pragma unroll
-  for (int t = 0; t < NT1; t++) b1v[t] = B1[32 * t + li];
-  // B operands of L2: W2[c = KS2*h + s][n = 32u + li] (half h contracts the
-  // contiguous channels [KS2*h, KS2*h + KS2): its A operands are 16-B reads)
-  float w2f[KS2][NT2];
-  float b2v[NT2];
+  for (int t = 0; t < NT1; t++)
 #pragma unroll
-  for (int s = 0; s < KS2; s++)
-#pragma unroll
-    for (int u = 0; u < NT2; u++) {
-      const int n = 32 * u + li;
-      w2f[s][u] = n < N2 ? W2[(KS2 * h + s) * N2 + n] : 0.0f;
-    }
-#pragma unroll
-  for (int u = 0; u < NT2; u++) b2v[u] = (32 * u + li) < N2 ? B2[32 * u + li] : 0.0f;
+    for (int s = 0; s < 16; s++) w2f[t][s] = li < N2 ? W2[(32 * t + crow(s, h)) * N2 + li] : 0.0f;
+  const float b2a = (h == 0 && li < N2) ? B2[li] : 0.0f;
 
   // The next sample's X tile is register-staged during the current sample
   // (its loads retire under the MFMAs instead of stalling both barriers);
-  // the LDS copy uses a fixed row stride so every L1 A operand is a per-half
+  // the LDS copy uses a fixed row stride so every L1 B operand is a per-half
   // base + immediate (tap 2s+1 sits 1 or kL12S - F1 + 1 floats past tap 2s).
   for (int i = threadIdx.x; i < kL12Tile; i += blockDim.x) xs[i] = 0.0f;
   const int xn = g.W * g.H;
@@ -122,89 +120,77 @@ __global__ __launch_bounds__(256, 2) void l12_fwd_kernel(
     __syncthreads();
     if (sample + (int)gridDim.x < g.batch) xload(sample + gridDim.x);
 
+    // Software-pipelined stores: chunk c's A1 / A2 rows (12 16-B stores per
+    // lane) are issued one at a time inside chunk c+1's L1 MFMA stream, so
+    // the write traffic streams out under the matrix core instead of in a
+    // burst that stalls the wave between chunks.
+    constexpr int NST = 4 * NT1 + N2 / 8;  // 16-B stores per lane per chunk
+    f32x16 pa1[NT1], pa2 = zero16();
+#pragma unroll
+    for (int t = 0; t < NT1; t++) pa1[t] = zero16();
+    bool pok = false;  // this lane has a pending pixel
+    float* pa1p = A1;
+    float* pa2p = A2;
+    auto store_prev = [&](int k) {  // store k of the pending chunk (exec-masked)
+      if (pok) {
+        if (k < 4 * NT1) {
+          const int t = k / 4, q = k % 4;
+          *reinterpret_cast<float4*>(pa1p + 32 * t + 8 * q) =
+              make_float4(pa1[t][4 * q], pa1[t][4 * q + 1], pa1[t][4 * q + 2], pa1[t][4 * q + 3]);
+        } else {
+          const int q = k - 4 * NT1;
+          *reinterpret_cast<float4*>(pa2p + 8 * q) =
+              make_float4(fmaxf(pa2[4 * q], 0.0f), fmaxf(pa2[4 * q + 1], 0.0f),
+                          fmaxf(pa2[4 * q + 2], 0.0f), fmaxf(pa2[4 * q + 3], 0.0f));
+        }
+      }
+    };
     for (int c = wave; c < nch; c += 4) {
-      // this lane's own pixel (A-operand row li)
-      const int pc = min(c * 32 + li, npx - 1);
+      // this lane's pixel (B-operand column li)
+      const int pl = c * 32 + li;
+      const int pc = min(pl, npx - 1);
       const int iy = pc / g.ow, ix = pc - iy * g.ow;
       const int xbA = iy * kL12S + ix + h, xbB = xbA + h * (kL12S - F1);
 
       f32x16 acc1[NT1];
 #pragma unroll
       for (int t = 0; t < NT1; t++) acc1[t] = zero16();
+      constexpr int kStoreEvery = (KS1 - 1) / NST;
 #pragma unroll
       for (int s = 0; s < KS1; s++) {
         const int k0 = 2 * s;
         const int o0 = (k0 / F1) * kL12S + (k0 % F1);
-        const float a = xs[((k0 % F1) + 1 < F1 ? xbA : xbB) + o0];
+        float xv = xs[((k0 % F1) + 1 < F1 ? xbA : xbB) + o0];
+        if (s == KS1 - 1) xv = h ? 1.0f : xv;  // tap K1 = the bias slot
 #pragma unroll
-        for (int t = 0; t < NT1; t++) acc1[t] = mma(a, w1f[s][t], acc1[t]);
+        for (int t = 0; t < NT1; t++) acc1[t] = mma(w1f[s][t], xv, acc1[t]);
+        if (s % kStoreEvery == kStoreEvery - 1 && s / kStoreEvery < NST) store_prev(s / kStoreEvery);
       }
-
-      // epilogue L1: bias + ReLU (layer_uber_kernel.cl:88-95) into the
-      // per-wave LDS transpose (rows = the chunk's 32 pixels, HWC order).
-      // That image is both L2's A operand and the source of the A1 stores:
-      // the chunk's A1 rows are one contiguous run in HBM, written as
-      // 16-B-per-lane coalesced stores (N1/8 per lane instead of 16*NT1
-      // scattered dword stores), issued under the L2 MFMAs.
+      // ReLU (layer_uber_kernel.cl:88-95); the bias is already in
 #pragma unroll
-      for (int r = 0; r < 16; r++)
+      for (int t = 0; t < NT1; t++)
 #pragma unroll
-        for (int t = 0; t < NT1; t++)
-          ts[wave][crow(r, h)][32 * t + li] = fmaxf(acc1[t][r] + b1v[t], 0.0f);
-      __builtin_amdgcn_wave_barrier();
-      // L2 A operands: this lane's pixel, channels [KS2*h, KS2*h + KS2)
-      float a2v[KS2];
+        for (int r = 0; r < 16; r++) acc1[t][r] = fmaxf(acc1[t][r], 0.0f);
+      f32x16 acc2 = zero16();
+      acc2 = mma(b2a, 1.0f, acc2);
 #pragma unroll
-      for (int q = 0; q < KS2 / 4; q++) {
-        const float4 v = *reinterpret_cast<const float4*>(&ts[wave][li][KS2 * h + 4 * q]);
-        a2v[4 * q] = v.x;
-        a2v[4 * q + 1] = v.y;
-        a2v[4 * q + 2] = v.z;
-        a2v[4 * q + 3] = v.w;
-      }
-      // A1 stores: float4 f = 64 i + lane of the chunk is pixel f / (N1/4);
-      // fire-and-forget, they drain while the L2 MFMAs below run
-      constexpr int Q1 = N1 / 4, NS1 = 32 * Q1 / 64;
-      const int p0 = c * 32;  // first pixel of the chunk
-      float* a1c = A1 + ((size_t)sample * npx + p0) * N1;
-      const bool full = p0 + 32 <= npx;  // wave-uniform
+      for (int t = 0; t < NT1; t++)
 #pragma unroll
-      for (int i = 0; i < NS1; i++) {
-        const int f = 64 * i + lane;
-        const float4 v = *reinterpret_cast<const float4*>(&ts[wave][f / Q1][4 * (f % Q1)]);
-        if (full || p0 + f / Q1 < npx)
-          *reinterpret_cast<float4*>(a1c + (size_t)(f / Q1) * N1 + 4 * (f % Q1)) = v;
-      }
-      f32x16 acc2[NT2];
+        for (int s = 0; s < 16; s++) acc2 = mma(w2f[t][s], acc1[t][s], acc2);
+      // this chunk becomes the pending one; registers 4q..4q+3 of tile t are
+      // channels 32t + 8q + 4h .. +3 of pixel pl
 #pragma unroll
-      for (int u = 0; u < NT2; u++) acc2[u] = zero16();
-#pragma unroll
-      for (int s = 0; s < KS2; s++)
-#pragma unroll
-        for (int u = 0; u < NT2; u++) acc2[u] = mma(a2v[s], w2f[s][u], acc2[u]);
-      // epilogue L2: bias + ReLU into the same transpose (columns 0..N2-1),
-      // then the chunk's A2 rows as coalesced 16-B stores
-      __builtin_amdgcn_wave_barrier();
-#pragma unroll
-      for (int r = 0; r < 16; r++)
-#pragma unroll
-        for (int u = 0; u < NT2; u++)
-          if (32 * u + li < N2) ts[wave][crow(r, h)][32 * u + li] = fmaxf(acc2[u][r] + b2v[u], 0.0f);
-      __builtin_amdgcn_wave_barrier();
-      constexpr int Q2 = N2 / 4, NS2 = (32 * Q2 + 63) / 64;
-      float* a2c = A2 + ((size_t)sample * npx + p0) * N2;
-#pragma unroll
-      for (int i = 0; i < NS2; i++) {
-        const int f = 64 * i + lane;
-        if (f < 32 * Q2 && (full || p0 + f / Q2 < npx))
-          *reinterpret_cast<float4*>(a2c + (size_t)(f / Q2) * N2 + 4 * (f % Q2)) =
-              *reinterpret_cast<const float4*>(&ts[wave][f / Q2][4 * (f % Q2)]);
-      }
-      __builtin_amdgcn_wave_barrier();
+      for (int t = 0; t < NT1; t++) pa1[t] = acc1[t];
+      pa2 = acc2;
+      pok = pl < npx;
+      pa1p = A1 + ((size_t)sample * npx + pc) * N1 + 4 * h;
+      pa2p = A2 + ((size_t)sample * npx + pc) * N2 + 4 * h;
     }
+#pragma unroll
+    for (int k = 0; k < NST; k++) store_prev(k);
+    pok = false;
   }
 }
-
 
 #include "l3_delta.hpp"
 
