@@ -55,45 +55,44 @@ __global__ __launch_bounds__(256, 2) void fwd_l123_kernel(
   constexpr int NT2 = (N2 + 31) / 32, KS2 = N1 / 2, KC = N2 / 2;
   constexpr int K3 = F3 * F3;
   constexpr int TW = kFwdRW + F1 - 1;  // LDS row stride of the input tile
-  constexpr int TS = N1 + 1;           // per-wave transpose row (A1, A2, then Q)
+  constexpr int QS = 36;               // Q row: 32 taps + pad, 16-B aligned
   constexpr int EW = kFwdRW + F3 - 1;  // partial-sum window width
   constexpr int EHM = kFwdRhMax + F3 - 1;
-  static_assert(K3 <= 32 && N2 <= 32 && N2 % 2 == 0, "Q tile shape");
+  static_assert(K3 <= 32 && N2 <= 32 && N2 % 2 == 0 && K1 % 2 == 1, "Q tile shape");
   __shared__ float xs[kFwdXs];
-  __shared__ float ts[4][32][TS];
-  __shared__ float w3s[32][N2 + 1];   // W3[tap][c] (taps >= K3 zero), padded rows
+  __shared__ __attribute__((aligned(16))) float qs[4][32][QS];  // per-wave Q[pixel][tap]
   __shared__ float accs[F3][EHM][EW];  // [dy][partial row][partial col]
 
   const int lane = mfma::lane_id(), wave = mfma::wave_id();
   const int h = lane >> 5, li = lane & 31;
   const int EH = g.rh + F3 - 1;
 
-  // B operands: W1[tap = 2s+h][32t+li], W2[c = 2s+h][32u+li], W3[tap = li][c = 2s+h]
+  // All three GEMMs run TRANSPOSED (rows = channels / taps, cols = the
+  // chunk's 32 pixels), so each layer's accumulator registers are the next
+  // layer's B operand as they stand (register s of half h is row crow(s, h),
+  // mfma.hpp) -- no LDS transposes between L1, L2 and Q:
+  //   A operands: W1[tap = 2s+h][ch = 32t+li] (tap K1 = the bias slot, X = 1),
+  //               W2[c = 32t + crow(s,h)][n = li] (+ one bias MFMA),
+  //               W3[tap = li][c = crow(s,h)]
   float w1f[KS1][NT1];
 #pragma unroll
   for (int s = 0; s < KS1; s++)
 #pragma unroll
     for (int t = 0; t < NT1; t++) {
       const int tap = 2 * s + h;
-      w1f[s][t] = tap < K1 ? W1[tap * N1 + 32 * t + li] : 0.0f;
+      w1f[s][t] = tap < K1 ? W1[tap * N1 + 32 * t + li] : B1[32 * t + li];
     }
-  float b1v[NT1];
+  float w2f[NT1][16];
 #pragma unroll
-  for (int t = 0; t < NT1; t++) b1v[t] = B1[32 * t + li];
-  float w2f[KS2][NT2];
+  for (int t = 0; t < NT1; t++)
 #pragma unroll
-  for (int s = 0; s < KS2; s++)
+    for (int s = 0; s < 16; s++) w2f[t][s] = li < N2 ? W2[(32 * t + crow(s, h)) * N2 + li] : 0.0f;
+  const float b2a = (h == 0 && li < N2) ? B2[li] : 0.0f;
+  float w3f[16];
 #pragma unroll
-    for (int u = 0; u < NT2; u++) {
-      const int n = 32 * u + li;
-      w2f[s][u] = n < N2 ? W2[(2 * s + h) * N2 + n] : 0.0f;
-    }
-  float b2v[NT2];
-#pragma unroll
-  for (int u = 0; u < NT2; u++) b2v[u] = (32 * u + li) < N2 ? B2[32 * u + li] : 0.0f;
-  for (int i = threadIdx.x; i < 32 * N2; i += 256) {
-    const int tap = i / N2, c = i - tap * N2;
-    w3s[tap][c] = tap < K3 ? W3[i] : 0.0f;
+  for (int s = 0; s < 16; s++) {
+    const int cc = crow(s, h);
+    w3f[s] = (li < K3 && cc < N2) ? W3[li * N2 + cc] : 0.0f;
   }
 
   const int per_frame = g.nrx * g.nry;
@@ -123,48 +122,34 @@ __global__ __launch_bounds__(256, 2) void fwd_l123_kernel(
         const int k0 = 2 * s, k1 = 2 * s + 1;
         const int o0 = (k0 / F1) * TW + (k0 % F1);
         const int o1 = k1 < K1 ? (k1 / F1) * TW + (k1 % F1) : 0;
-        const float a = xs[xb + (h ? o1 : o0)];
+        float xv = xs[xb + (h ? o1 : o0)];
+        if (s == KS1 - 1) xv = h ? 1.0f : xv;  // tap K1 = the bias slot
 #pragma unroll
-        for (int t = 0; t < NT1; t++) acc1[t] = mma(a, w1f[s][t], acc1[t]);
+        for (int t = 0; t < NT1; t++) acc1[t] = mma(w1f[s][t], xv, acc1[t]);
       }
-      // L1 bias + ReLU -> transpose (A operand of L2)
+      // L1 ReLU (layer_uber_kernel.cl:88-95; bias already in)
 #pragma unroll
-      for (int r = 0; r < 16; r++)
+      for (int t = 0; t < NT1; t++)
 #pragma unroll
-        for (int t = 0; t < NT1; t++)
-          ts[wave][crow(r, h)][32 * t + li] = fmaxf(acc1[t][r] + b1v[t], 0.0f);
-      __builtin_amdgcn_wave_barrier();
-      f32x16 acc2[NT2];
+        for (int r = 0; r < 16; r++) acc1[t][r] = fmaxf(acc1[t][r], 0.0f);
+      // L2^T: A2^T[n][p] = B2[n] + sum_c W2[c][n] A1^T[c][p], then ReLU
+      f32x16 acc2 = zero16();
+      acc2 = mma(b2a, 1.0f, acc2);
 #pragma unroll
-      for (int u = 0; u < NT2; u++) acc2[u] = zero16();
+      for (int t = 0; t < NT1; t++)
 #pragma unroll
-      for (int s = 0; s < KS2; s++) {
-        const float a = ts[wave][li][2 * s + h];
+        for (int s = 0; s < 16; s++) acc2 = mma(w2f[t][s], acc1[t][s], acc2);
 #pragma unroll
-        for (int u = 0; u < NT2; u++) acc2[u] = mma(a, w2f[s][u], acc2[u]);
-      }
-      // L2 bias + ReLU -> the same transpose (its L2 reads have retired)
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_wave_barrier();
-#pragma unroll
-      for (int r = 0; r < 16; r++)
-#pragma unroll
-        for (int u = 0; u < NT2; u++) {
-          const int nn = 32 * u + li;
-          if (nn < N2) ts[wave][crow(r, h)][nn] = fmaxf(acc2[u][r] + b2v[u], 0.0f);
-        }
-      __builtin_amdgcn_wave_barrier();
-      // Q = A2 . W3^T for the chunk's 32 pixels
+      for (int r = 0; r < 16; r++) acc2[r] = fmaxf(acc2[r], 0.0f);
+      // Q^T[tap][p] = sum_c W3[tap][c] A2^T[c][p]
       f32x16 accq = zero16();
 #pragma unroll
-      for (int s = 0; s < KC; s++) accq = mma(ts[wave][li][2 * s + h], w3s[li][2 * s + h], accq);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_wave_barrier();
-      // Q[pixel][tap] -> the transpose rows (lane = tap)
-      if (li < K3) {
+      for (int s = 0; s < 16; s++) accq = mma(w3f[s], acc2[s], accq);
+      // Q[pixel li][taps crow(r, h)]: 4 runs of 4 consecutive taps per lane
 #pragma unroll
-        for (int r = 0; r < 16; r++) ts[wave][crow(r, h)][li] = accq[r];
-      }
+      for (int q = 0; q < 4; q++)
+        *reinterpret_cast<float4*>(&qs[wave][li][8 * q + 4 * h]) =
+            make_float4(accq[4 * q], accq[4 * q + 1], accq[4 * q + 2], accq[4 * q + 3]);
       __builtin_amdgcn_wave_barrier();
       // tap row dy of this chunk feeds partial row c + F3 - 1 - dy:
       //   accs[dy][c + F3-1 - dy][e] = sum_dx Q[e - (F3-1) + dx][dy*F3 + dx]
@@ -174,7 +159,7 @@ __global__ __launch_bounds__(256, 2) void fwd_l123_kernel(
 #pragma unroll
         for (int dx = 0; dx < F3; dx++) {
           const int px = e - (F3 - 1) + dx;
-          if (px >= 0 && px < kFwdRW) v += ts[wave][px][dy * F3 + dx];
+          if (px >= 0 && px < kFwdRW) v += qs[wave][px][dy * F3 + dx];
         }
         accs[dy][c + F3 - 1 - dy][e] = v;
       }
