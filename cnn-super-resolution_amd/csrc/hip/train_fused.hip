@@ -235,7 +235,7 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
   constexpr int MT = K1 / 16;             // 16-tap MFMA tiles
   constexpr int KR = K1 - 16 * MT;        // taps left to the VALU
   constexpr int KD = N2 / 4;              // delta1 k-steps (over n)
-  constexpr int DS = N2 + 1;              // padded delta2 row in LDS
+  constexpr int DS = N2 + 4;              // delta2 row in LDS: N2/4 quads + 1 pad quad
   constexpr int WS = N2 + 1;              // padded W2 row in LDS
   constexpr int A1P = N1 + 4;             // padded A1 row of the LDS image
   constexpr int NW1 = K1 * N1, NW2 = N1 * N2;
@@ -246,8 +246,8 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
   constexpr int A1K = (32 * A1P + 255) / 256;  // 16-byte DMA instructions per A1 chunk
   constexpr int A1S = 256 * A1K;               // per-wave A1 staging
   constexpr int D2S = 32 * DS;                 // per-wave delta2 chunk image [32][DS]
-  constexpr int D2K = (D2S + 63) / 64;         // 4-byte DMA instructions per chunk
-  constexpr int D2P = 64 * D2K;                // per-wave staging stride (whole DMA instructions)
+  constexpr int D2K = (D2S + 255) / 256;       // 16-byte DMA instructions per chunk
+  constexpr int D2P = 256 * D2K;               // per-wave staging stride (whole DMA instructions)
   constexpr int LDS_MAIN = 4 * A1S + 2 * kXsMax + N1 * WS + 4 * D2P;
   constexpr int LDS_TOTAL = LDS_MAIN > RED ? LDS_MAIN : RED;
   __shared__ __attribute__((aligned(16))) float smem[LDS_TOTAL];
@@ -299,9 +299,10 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
   // One LDS-DMA instruction K of a chunk's operands (no registers):
   //   K < A1K: A1 rows -> this wave's lane-linear [32][A1P] image (16 B / lane;
   //            the 4-float pad of each row re-reads its first quad)
-  //   K >= A1K: delta2 rows -> this wave's padded [32][DS] image (4 B / lane;
-  //            the pad column re-reads col 0, lanes past the image write into
-  //            the staging padding)
+  //   K >= A1K: delta2 rows -> this wave's padded [32][DS] image (16 B / lane;
+  //            the pad quad re-reads quad 0, lanes past the image write into
+  //            the staging padding; 2-way bank conflicts on the 16 delta1
+  //            operand reads per chunk, 13 fewer DMA instructions)
   // Rows past the sample re-read its last row (A1: finite, and the delta2
   // rows there are zeroed in LDS before use).
   constexpr int kDmaK = A1K + D2K;
@@ -321,12 +322,14 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
           (const void*)(A1 + px0_ * N1 + off_),                                   \
           (__attribute__((address_space(3))) void*)(a1me + (K) * 256), 16, 0, 0); \
     } else {                                                                      \
-      const uint32_t f_ = 64 * ((K) - A1K) + (uint32_t)l_;                        \
-      const uint32_t r_ = f_ / DS, col_ = f_ - r_ * DS;                           \
-      const uint32_t off_ = (uint32_t)min((int)r_, rmax_) * N2 + (col_ < N2 ? col_ : 0u); \
+      /* delta2 rows, 16 B / lane: slot quad Q of the [32][DS] image is row */   \
+      /* Q / (DS/4), quad Q % (DS/4); the pad quad re-reads quad 0 */            \
+      const uint32_t q_ = 64 * ((K) - A1K) + (uint32_t)l_;                        \
+      const uint32_t r_ = q_ / (DS / 4), j_ = q_ - r_ * (DS / 4);                 \
+      const uint32_t off_ = (uint32_t)min((int)r_, rmax_) * N2 + (j_ < N2 / 4 ? 4 * j_ : 0u); \
       __builtin_amdgcn_global_load_lds(                                           \
           (const void*)(D2 + px0_ * N2 + off_),                                   \
-          (__attribute__((address_space(3))) void*)(d2me + 64 * ((K) - A1K)), 4, 0, 0); \
+          (__attribute__((address_space(3))) void*)(d2me + 256 * ((K) - A1K)), 16, 0, 0); \
     }                                                                             \
   } while (0)
 #define SRCNN_D1_DMA_ALL(SMP, C)                                                  \
