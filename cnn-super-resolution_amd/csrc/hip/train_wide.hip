@@ -261,10 +261,17 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restri
     }
   };
   int abase[MT];
+  // delta1: a tap row dy whose image rows are zero border for every pixel of
+  // tile m (dy outside [dlo, dhi]) is skipped for that tile (wave-uniform
+  // branches around MFMA groups that hold no memory operations)
+  int dlo[MT], dhi[MT];
 #pragma unroll
   for (int m = 0; m < MT; m++) {
     const int o = min(32 * (mg * MT + m) + j, g.npx - 1), oy = o / g.out_w;
     abase[m] = (oy * g.img_w + o - oy * g.out_w) * kPS + 4 * h;
+    const int pa = min(32 * (mg * MT + m), g.npx - 1), pb = min(pa + 31, g.npx - 1);
+    dlo[m] = __builtin_amdgcn_readfirstlane(g.pad - pb / g.out_w);
+    dhi[m] = __builtin_amdgcn_readfirstlane(g.pad + g.in_h - 1 - pa / g.out_w);
   }
   // one LDS-DMA instruction k (64 slots of 16 B) of chunk c of item it
   auto dma = [&](int it, int c, float* buf, int k) {
@@ -340,18 +347,22 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restri
             an[m] = *reinterpret_cast<const float4*>(cur + abase[m] + toff + 8);
           __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-          for (int jj = 0; jj < 4; jj++)
+          for (int m = 0; m < MT; m++)
+            if (!DELTA || (dy >= dlo[m] && dy <= dhi[m])) {
 #pragma unroll
-            for (int m = 0; m < MT; m++) acc[m] = mma(a[m][jj], bq[dx][0][jj], acc[m]);
+              for (int jj = 0; jj < 4; jj++) acc[m] = mma(a[m][jj], bq[dx][0][jj], acc[m]);
+            }
           __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
           for (int m = 0; m < MT; m++)
             a[m] = *reinterpret_cast<const float4*>(cur + abase[m] + toffn);
           __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-          for (int jj = 0; jj < 4; jj++)
+          for (int m = 0; m < MT; m++)
+            if (!DELTA || (dy >= dlo[m] && dy <= dhi[m])) {
 #pragma unroll
-            for (int m = 0; m < MT; m++) acc[m] = mma(an[m][jj], bq[dx][1][jj], acc[m]);
+              for (int jj = 0; jj < 4; jj++) acc[m] = mma(an[m][jj], bq[dx][1][jj], acc[m]);
+            }
           __builtin_amdgcn_sched_barrier(0);
         }
       }
