@@ -192,7 +192,8 @@ __global__ void prepack_w2_kernel(const float* __restrict__ W2, float* __restric
 //   delta1  (DELTA = true):  img = delta2 zero-padded by F-1, W flipped and
 //                            transposed, epi = [A1 > 0] * v     (layer_deltas.cl)
 // Work item = (sample, 64 output channels).  4 waves: wave = (N tile nt of 32
-// channels, M group mg of MT 32-pixel tiles); the whole item's accumulators
+// channels, M group mg: the MT 32-pixel tiles 2m + mg, interleaved so both
+// groups skip equally many border tap rows in delta1); the whole item's accumulators
 // live in registers across the K loop (CIN/16 chunks x F*F taps x 2).
 // Each chunk's image (img_w x img_h pixels x 16 channels, 80-B rows) is
 // staged by LDS-DMA into the other buffer while the current one is consumed;
@@ -267,9 +268,9 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restri
   int dlo[MT], dhi[MT];
 #pragma unroll
   for (int m = 0; m < MT; m++) {
-    const int o = min(32 * (mg * MT + m) + j, g.npx - 1), oy = o / g.out_w;
+    const int o = min(32 * (2 * m + mg) + j, g.npx - 1), oy = o / g.out_w;
     abase[m] = (oy * g.img_w + o - oy * g.out_w) * kPS + 4 * h;
-    const int pa = min(32 * (mg * MT + m), g.npx - 1), pb = min(pa + 31, g.npx - 1);
+    const int pa = min(32 * (2 * m + mg), g.npx - 1), pb = min(pa + 31, g.npx - 1);
     dlo[m] = __builtin_amdgcn_readfirstlane(g.pad - pb / g.out_w);
     dhi[m] = __builtin_amdgcn_readfirstlane(g.pad + g.in_h - 1 - pa / g.out_w);
   }
@@ -379,18 +380,18 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restri
       float mk[16], mkn[16];
 #pragma unroll
       for (int r = 0; r < 16; r++) {
-        const int pix = min(32 * mg * MT + crow(r, h), g.npx - 1);
+        const int pix = min(32 * mg + crow(r, h), g.npx - 1);
         mk[r] = ycur[obase + (size_t)pix * COUT];
       }
 #pragma unroll
       for (int m = 0; m < MT; m++) {
         int hl = h;
         asm volatile("" : "+v"(hl));
-        const int p0 = 32 * (mg * MT + m) + 4 * hl;
+        const int p0 = 32 * (2 * m + mg) + 4 * hl;
         if (m + 1 < MT) {
 #pragma unroll
           for (int r = 0; r < 16; r++) {
-            const int pix = min(p0 + 32 + crow(r, 0), g.npx - 1);
+            const int pix = min(p0 + 64 + crow(r, 0), g.npx - 1);
             mkn[r] = ycur[obase + (size_t)pix * COUT];
           }
         }
@@ -422,7 +423,7 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restri
       for (int m = 0; m < MT; m++) {
         int hl = h;
         asm volatile("" : "+v"(hl));
-        const int p0 = 32 * (mg * MT + m) + 4 * hl;
+        const int p0 = 32 * (2 * m + mg) + 4 * hl;
 #pragma unroll
         for (int r = 0; r < 16; r++) {
           const int pix = p0 + crow(r, 0);
