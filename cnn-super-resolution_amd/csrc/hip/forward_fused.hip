@@ -35,8 +35,14 @@ using mfma::zero16;
 namespace {
 
 constexpr int kFwdRW = 32;        // region width (one chunk per region row)
-constexpr int kFwdXs = 1536;      // input tile floats staged in LDS
-constexpr int kFwdRhMax = 28;     // region rows (LDS partial-sum accumulator bound)
+#ifndef SRCNN_FWD_RH
+#define SRCNN_FWD_RH 28
+#endif
+#ifndef SRCNN_FWD_GRID
+#define SRCNN_FWD_GRID 2048
+#endif
+constexpr int kFwdRhMax = SRCNN_FWD_RH;  // region rows (LDS partial-sum accumulator bound)
+constexpr int kFwdXs = (kFwdRhMax + 12) * 40;  // input tile floats staged in LDS (f1 <= 9)
 
 struct FwdGeom {
   int W, H;      // input frame
@@ -220,7 +226,7 @@ int run_forward(const float* X, uint32_t w, uint32_t h, uint32_t batch, const fl
   if (ow < F3 || oh < F3) return 0;
   // region rows: the input tile (32 + f1 - 1) x (rh + f1 - 1) fits the LDS tile,
   // a multiple of the 4 waves
-  int rh = std::min((kFwdXs / (kFwdRW + F1 - 1) - (F1 - 1)) / 4 * 4, kFwdRhMax);
+  int rh = std::min((kFwdXs / (kFwdRW + F1 - 1) - (F1 - 1)) / 4 * 4, kFwdRhMax / 4 * 4);
   if (rh < F3) return 0;
   rh = std::min(rh, oh);
   FwdGeom g{(int)w, (int)h, ow, oh, rh, (ow + kFwdRW - 1) / kFwdRW, (oh + rh - 1) / rh, (int)batch};
@@ -241,7 +247,7 @@ int run_forward(const float* X, uint32_t w, uint32_t h, uint32_t batch, const fl
   const float* B3 = W3 + F3 * F3 * N2;
   {
     SRCNN_PROFILE("fwd_l123_mfma", s);
-    hipLaunchKernelGGL((fwd_l123_kernel<N1, N2, F1, F3>), dim3((unsigned)std::min<long>(items, 2048)),
+    hipLaunchKernelGGL((fwd_l123_kernel<N1, N2, F1, F3>), dim3((unsigned)std::min<long>(items, SRCNN_FWD_GRID)),
                        dim3(256), 0, s, X, W1, B1, W2, B2, W3, part, g);
     SRCNN_LAUNCH_TRY();
   }

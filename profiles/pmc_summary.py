@@ -22,6 +22,8 @@ SHORT = [
     (r"l3_delta_kernel", "l3_delta_fused"),
     (r"d1_grad12_kernel", "delta1_grad12_fused"),
     (r"slab_reduce_kernel", "slab_reduce"),
+    (r"fwd_l123_kernel", "fwd_l123_mfma"),
+    (r"fwd_seam_kernel", "fwd_l3_seam"),
     (r"wide::prepack_w2_kernel", "wide_prepack_w2"),
     (r"wide::wl1_fwd_kernel", "wide_l1_fwd"),
     (r"wide::conv_mfma_kernel<128, 64", "wide_l2_fwd"),
