@@ -119,16 +119,17 @@ __global__ __launch_bounds__(256, 2) void fwd_l123_kernel(
     __syncthreads();
 
     for (int c = wave; c < crh; c += 4) {  // chunk = region row c, pixel li
-      const int xb = c * TW + li;
+      // tap 2s+1 sits 1 or TW - F1 + 1 floats past tap 2s: two per-half bases,
+      // every gather is base + immediate
+      const int xbA = c * TW + li + h, xbB = xbA + h * (TW - F1);
       f32x16 acc1[NT1];
 #pragma unroll
       for (int t = 0; t < NT1; t++) acc1[t] = zero16();
 #pragma unroll
       for (int s = 0; s < KS1; s++) {
-        const int k0 = 2 * s, k1 = 2 * s + 1;
+        const int k0 = 2 * s;
         const int o0 = (k0 / F1) * TW + (k0 % F1);
-        const int o1 = k1 < K1 ? (k1 / F1) * TW + (k1 % F1) : 0;
-        float xv = xs[xb + (h ? o1 : o0)];
+        float xv = xs[((k0 % F1) + 1 < F1 ? xbA : xbB) + o0];
         if (s == KS1 - 1) xv = h ? 1.0f : xv;  // tap K1 = the bias slot
 #pragma unroll
         for (int t = 0; t < NT1; t++) acc1[t] = mma(w1f[s][t], xv, acc1[t]);
