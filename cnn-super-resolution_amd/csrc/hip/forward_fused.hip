@@ -38,6 +38,9 @@ constexpr int kFwdRW = 32;        // region width (one chunk per region row)
 #ifndef SRCNN_FWD_RH
 #define SRCNN_FWD_RH 28
 #endif
+#ifndef SRCNN_FWD_WAVES
+#define SRCNN_FWD_WAVES 2  // minimum waves per SIMD (register budget 512 / this)
+#endif
 #ifndef SRCNN_FWD_GRID
 #define SRCNN_FWD_GRID 2048
 #endif
@@ -53,7 +56,7 @@ struct FwdGeom {
 };
 
 template <int N1, int N2, int F1, int F3>
-__global__ __launch_bounds__(256, 2) void fwd_l123_kernel(
+__global__ __launch_bounds__(256, SRCNN_FWD_WAVES) void fwd_l123_kernel(
     const float* __restrict__ X, const float* __restrict__ W1, const float* __restrict__ B1,
     const float* __restrict__ W2, const float* __restrict__ B2, const float* __restrict__ W3,
     float* __restrict__ part, FwdGeom g) {
