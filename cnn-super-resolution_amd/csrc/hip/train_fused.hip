@@ -37,9 +37,18 @@ using mfma::mma;
 using mfma::zero16;
 
 constexpr int kXsMax = 1536;  // input sample / region tile (floats) staged in LDS (<= 39x39)
-constexpr int kL12S = 40;                     // l12_fwd X tile row stride (w, h <= 40)
-constexpr int kL12Tile = kL12S * (kL12S + 1);  // + a zero row read by the padded tap
-constexpr int kL12Regs = (kL12S * kL12S + 255) / 256;
+// l12_fwd X tile in LDS: rows at the fixed stride kL12S (w <= kL12S, h <= kL12Rows).
+// A chunk's 32 consecutive L1 pixels (flattened over ow) gather from banks
+// (row * kL12S + col) mod 32 (ds_read_b32 banks 32 lanes at a time), which
+// is (pixel index + const) mod 32 -- 32 distinct banks -- when kL12S == ow
+// (mod 32): 57 = 25 + 32 makes the default 33x33 tile (ow 25) conflict-free.
+#ifndef SRCNN_L12_S
+#define SRCNN_L12_S 57
+#endif
+constexpr int kL12S = SRCNN_L12_S;
+constexpr int kL12Rows = 40;
+constexpr int kL12Tile = kL12S * (kL12Rows + 1);  // + a zero row read by the padded tap
+constexpr int kL12Regs = (kXsMax + 255) / 256;    // register-staged X tile (w * h <= kXsMax)
 
 struct Geom {
   int W, H;      // input sample
@@ -59,8 +68,17 @@ struct Geom {
 //         mfma.hpp), A = W2 (registers); one extra MFMA adds B2
 // so L2 needs no LDS transpose at all, and each lane ends with consecutive
 // channels of ONE pixel: A1 / A2 leave as 16-B stores straight from registers.
+#ifndef SRCNN_L12_W1LDS
+#define SRCNN_L12_W1LDS 0
+#endif
+#ifndef SRCNN_L12_GRID
+#define SRCNN_L12_GRID 1024  // grid cap (blocks), a multiple of 256 CUs x blocks per CU
+#endif
+#ifndef SRCNN_L12_WAVES
+#define SRCNN_L12_WAVES 2  // minimum waves per SIMD (register budget 512 / this)
+#endif
 template <int N1, int N2, int F1>
-__global__ __launch_bounds__(256, 2) void l12_fwd_kernel(
+__global__ __launch_bounds__(256, SRCNN_L12_WAVES) void l12_fwd_kernel(
     const float* __restrict__ X, const float* __restrict__ W1, const float* __restrict__ B1,
     const float* __restrict__ W2, const float* __restrict__ B2, float* __restrict__ A1,
     float* __restrict__ A2, Geom g) {
@@ -75,6 +93,15 @@ __global__ __launch_bounds__(256, 2) void l12_fwd_kernel(
   const int nch = (npx + 31) / 32;
 
   // A operands of L1^T: W1[tap = 2s + h][ch = 32t + li]; tap K1 is the bias slot
+#if SRCNN_L12_W1LDS
+  // read from LDS at each MFMA (frees 2 * KS1 registers for a third wave per SIMD)
+  __shared__ float w1s[2 * KS1 * N1];
+  for (int i = threadIdx.x; i < 2 * KS1 * N1; i += blockDim.x) {
+    const int tap = i / N1, ch = i - tap * N1;
+    w1s[i] = tap < K1 ? W1[i] : (tap == K1 ? B1[ch] : 0.0f);
+  }
+#define SRCNN_W1F(S, T) w1s[w1o + 2 * (S) * N1 + 32 * (T)]
+#else
   float w1f[KS1][NT1];
 #pragma unroll
   for (int s = 0; s < KS1; s++)
@@ -83,6 +110,8 @@ __global__ __launch_bounds__(256, 2) void l12_fwd_kernel(
       const int tap = 2 * s + h;
       w1f[s][t] = tap < K1 ? W1[tap * N1 + 32 * t + li] : B1[32 * t + li];
     }
+#define SRCNN_W1F(S, T) w1f[S][T]
+#endif
   // A operands of L2^T: W2[c = 32t + crow(s, h)][n = li]; bias MFMA: B2[li] (half 0)
   float w2f[NT1][16];
 #pragma unroll
@@ -152,6 +181,11 @@ __global__ __launch_bounds__(256, 2) void l12_fwd_kernel(
       const int iy = pc / g.ow, ix = pc - iy * g.ow;
       const int xbA = iy * kL12S + ix + h, xbB = xbA + h * (kL12S - F1);
 
+#if SRCNN_L12_W1LDS
+      // opaque per chunk, so the W1 reads are not hoisted out of the loops
+      int w1o = h * N1 + li;
+      asm volatile("" : "+v"(w1o));
+#endif
       f32x16 acc1[NT1];
 #pragma unroll
       for (int t = 0; t < NT1; t++) acc1[t] = zero16();
@@ -163,7 +197,7 @@ __global__ __launch_bounds__(256, 2) void l12_fwd_kernel(
         float xv = xs[((k0 % F1) + 1 < F1 ? xbA : xbB) + o0];
         if (s == KS1 - 1) xv = h ? 1.0f : xv;  // tap K1 = the bias slot
 #pragma unroll
-        for (int t = 0; t < NT1; t++) acc1[t] = mma(w1f[s][t], xv, acc1[t]);
+        for (int t = 0; t < NT1; t++) acc1[t] = mma(SRCNN_W1F(s, t), xv, acc1[t]);
         if (s % kStoreEvery == kStoreEvery - 1 && s / kStoreEvery < NST) store_prev(s / kStoreEvery);
       }
       // ReLU (layer_uber_kernel.cl:88-95); the bias is already in
@@ -191,6 +225,7 @@ __global__ __launch_bounds__(256, 2) void l12_fwd_kernel(
     pok = false;
   }
 }
+#undef SRCNN_W1F
 
 #include "l3_delta.hpp"
 
@@ -671,10 +706,10 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   using NetT = Net<N1, N2, F1, F3>;
   const int ow = w - F1 + 1, oh = h - F1 + 1;
   const int w3 = ow - F3 + 1, h3 = oh - F3 + 1;
-  if ((int)(w * h) > kXsMax || (int)w > kL12S || (int)h > kL12S || w3 <= 0 || h3 <= 0) return 0;
+  if ((int)(w * h) > kXsMax || (int)w > kL12S || (int)h > kL12Rows || w3 <= 0 || h3 <= 0) return 0;
   const size_t lds3 = l3_lds_bytes<N2, F3>(ow, oh);
   if (lds3 > 160 * 1024 || w3 * h3 > kL3MaxOut) return 0;
-  const int g12 = grid_for_batch(batch, 1024);
+  const int g12 = grid_for_batch(batch, SRCNN_L12_GRID);
   const int g3 = grid_for_batch(batch, 256);
   const int gd = grid_for_batch(batch, 512);
   const size_t s12 = (size_t)gd * NetT::P12, s3 = (size_t)g3 * NetT::P3;

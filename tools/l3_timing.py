@@ -8,7 +8,7 @@ import sys
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["SRCNN_HIP_LIB"] = os.path.join(ROOT, "cnn-super-resolution_amd/lib/variants/libsrcnn_hip_l3t.so")
+os.environ.setdefault("SRCNN_HIP_LIB", os.path.join(ROOT, "cnn-super-resolution_amd/lib/variants/libsrcnn_hip_l3t.so"))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "cnn-super-resolution_amd"), os.path.join(ROOT, "tests")]
 import torch  # noqa: E402
 import srcnn_amd as S  # noqa: E402
@@ -29,9 +29,11 @@ for _ in range(3):
 torch.cuda.synchronize()
 buf = (ctypes.c_ulonglong * (1024 * 4))()
 assert S.lib().srcnn_debug_l3_timing(buf) == 0
-t = np.array(buf, dtype=np.float64).reshape(1024, 4)[:256]
+t = np.array(buf, dtype=np.float64).reshape(1024, 4)
+t = t[t.sum(axis=1) > 0]
+spb = B / len(t)  # samples per block
 names = ["Q mfma", "L3 gather+delta3", "delta2+gW3 (wave 0)", "top wait (DMA+barrier)"]
 tot = t.sum(axis=1).mean()
 for i, n in enumerate(names):
-    print("%-18s %10.0f cycles/block  %5.1f%%  (%.0f per sample)" % (n, t[:, i].mean(), 100 * t[:, i].mean() / tot, t[:, i].mean() / 16))
-print("total %.0f cycles/block = %.1f us at 2.2 GHz" % (tot, tot / 2.2e3))
+    print("%-18s %10.0f cycles/block  %5.1f%%  (%.0f per sample)" % (n, t[:, i].mean(), 100 * t[:, i].mean() / tot, t[:, i].mean() / spb))
+print("%d blocks, total %.0f cycles/block = %.1f us at 2.2 GHz" % (len(t), tot, tot / 2.2e3))
