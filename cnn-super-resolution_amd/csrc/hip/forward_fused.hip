@@ -61,7 +61,6 @@ __global__ __launch_bounds__(256, SRCNN_FWD_WAVES) void fwd_l123_kernel(
     const float* __restrict__ W2, const float* __restrict__ B2, const float* __restrict__ W3,
     float* __restrict__ part, FwdGeom g) {
   constexpr int K1 = F1 * F1, KS1 = (K1 + 1) / 2, NT1 = N1 / 32;
-  constexpr int NT2 = (N2 + 31) / 32, KS2 = N1 / 2, KC = N2 / 2;
   constexpr int K3 = F3 * F3;
   constexpr int TW = kFwdRW + F1 - 1;  // LDS row stride of the input tile
   constexpr int QS = 36;               // Q row: 32 taps + pad, 16-B aligned
@@ -106,20 +105,39 @@ __global__ __launch_bounds__(256, SRCNN_FWD_WAVES) void fwd_l123_kernel(
 
   const int per_frame = g.nrx * g.nry;
   const int n_items = g.batch * per_frame;
-  for (int wi = blockIdx.x; wi < n_items; wi += gridDim.x) {
+  // The next region's input tile is register-staged while this region's
+  // chunks run (its loads retire under the MFMAs instead of stalling the
+  // block between regions); rows / columns past the frame read as 0.
+  constexpr int kXR = (kFwdXs + 255) / 256;
+  float xr[kXR];
+  auto xload = [&](int wi) {
     const int n = wi / per_frame, rr = wi - n * per_frame;
     const int ry = rr / g.nrx, rx = rr - ry * g.nrx;
     const int oy0 = ry * g.rh, ox0 = rx * kFwdRW;
-    const int crh = min(g.rh, g.oh - oy0), crw = min(kFwdRW, g.ow - ox0);
-    const int th = crh + F1 - 1, tw = crw + F1 - 1;
+    const int th = min(g.rh, g.oh - oy0) + F1 - 1, tw = min(kFwdRW, g.ow - ox0) + F1 - 1;
+    const float* xsrc = X + (size_t)n * g.W * g.H + (size_t)oy0 * g.W + ox0;
+#pragma unroll
+    for (int k = 0; k < kXR; k++) {
+      const int i = threadIdx.x + 256 * k;
+      const int iy = i / TW, ix = i - iy * TW;
+      xr[k] = (i < th * TW && ix < tw) ? xsrc[(size_t)iy * g.W + ix] : 0.0f;
+    }
+  };
+  if ((int)blockIdx.x < n_items) xload(blockIdx.x);
+  for (int wi = blockIdx.x; wi < n_items; wi += gridDim.x) {
+    const int n = wi / per_frame, rr = wi - n * per_frame;
+    const int ry = rr / g.nrx;
+    const int oy0 = ry * g.rh;
+    const int crh = min(g.rh, g.oh - oy0);
 
     __syncthreads();  // the previous region's readers are done with xs / accs
-    const float* xsrc = X + (size_t)n * g.W * g.H + (size_t)oy0 * g.W + ox0;
-    for (int i = threadIdx.x; i < th * TW; i += 256) {
-      const int iy = i / TW, ix = i - iy * TW;
-      xs[i] = ix < tw ? xsrc[(size_t)iy * g.W + ix] : 0.0f;
+#pragma unroll
+    for (int k = 0; k < kXR; k++) {
+      const int i = threadIdx.x + 256 * k;
+      if (i < kFwdXs) xs[i] = xr[k];
     }
     __syncthreads();
+    if (wi + (int)gridDim.x < n_items) xload(wi + gridDim.x);
 
     for (int c = wave; c < crh; c += 4) {  // chunk = region row c, pixel li
       // tap 2s+1 sits 1 or TW - F1 + 1 floats past tap 2s: two per-half bases,
