@@ -44,6 +44,10 @@ constexpr int kFwdRW = 32;        // region width (one chunk per region row)
 #ifndef SRCNN_FWD_GRID
 #define SRCNN_FWD_GRID 2048
 #endif
+#ifndef SRCNN_FWD_PD
+#define SRCNN_FWD_PD 4  // L1 X-gather prefetch distance (k-steps); 0 = compiler schedule
+#endif
+constexpr int kFwdPD = SRCNN_FWD_PD;
 constexpr int kFwdRhMax = SRCNN_FWD_RH;  // region rows (LDS partial-sum accumulator bound)
 constexpr int kFwdXs = (kFwdRhMax + 12) * 40;  // input tile floats staged in LDS (f1 <= 9)
 
@@ -146,12 +150,24 @@ __global__ __launch_bounds__(256, SRCNN_FWD_WAVES) void fwd_l123_kernel(
       f32x16 acc1[NT1];
 #pragma unroll
       for (int t = 0; t < NT1; t++) acc1[t] = zero16();
-#pragma unroll
-      for (int s = 0; s < KS1; s++) {
+      // B operand of k-step s (tap K1 = the bias slot)
+      auto xg = [&](int s) {
         const int k0 = 2 * s;
         const int o0 = (k0 / F1) * TW + (k0 % F1);
-        float xv = xs[((k0 % F1) + 1 < F1 ? xbA : xbB) + o0];
-        if (s == KS1 - 1) xv = h ? 1.0f : xv;  // tap K1 = the bias slot
+        const float v = xs[((k0 % F1) + 1 < F1 ? xbA : xbB) + o0];
+        return s == KS1 - 1 ? (h ? 1.0f : v) : v;
+      };
+      // gathers run kFwdPD k-steps ahead of their MFMAs, pinned by sched
+      // barriers: left alone, the scheduler issues each one just before its
+      // MFMA pair and the wave waits out the full LDS latency every step
+      float xq[KS1];
+#pragma unroll
+      for (int s = 0; s < kFwdPD && s < KS1; s++) xq[s] = xg(s);
+#pragma unroll
+      for (int s = 0; s < KS1; s++) {
+        if (s + kFwdPD < KS1) xq[s + kFwdPD] = xg(s + kFwdPD);
+        if (kFwdPD > 0) __builtin_amdgcn_sched_barrier(0);
+        const float xv = kFwdPD > 0 ? xq[s] : xg(s);
 #pragma unroll
         for (int t = 0; t < NT1; t++) acc1[t] = mma(w1f[s][t], xv, acc1[t]);
       }

@@ -40,6 +40,23 @@ __device__ unsigned long long g_l3_timing[1024][4];
   } while (0)
 #endif
 
+// diagnostics builds only (results invalid): drop one part of the delta2 phase
+#ifdef SRCNN_L3_DIAG_NOSTORE
+constexpr bool kL3DiagNoStore = true;
+#else
+constexpr bool kL3DiagNoStore = false;
+#endif
+#ifdef SRCNN_L3_DIAG_NOD2
+constexpr bool kL3DiagNoD2 = true;
+#else
+constexpr bool kL3DiagNoD2 = false;
+#endif
+#ifdef SRCNN_L3_DIAG_NOGW3
+constexpr bool kL3DiagNoGW3 = true;
+#else
+constexpr bool kL3DiagNoGW3 = false;
+#endif
+
 struct L3Geom {
   int W, H;     // ground-truth sample (= network input size)
   int w2, h2;   // A2
@@ -61,13 +78,18 @@ __device__ __forceinline__ int a2_at(int p, int n) {
 // LDS geometry shared by host and device (floats)
 template <int N2, int F3>
 struct L3Lds {
-  int region;  // one ping-pong region: max(A2 tile, Q, reduction scratch)
+  // 16-pixel units per wave of the largest A2 tile whose two regions fit the
+  // 160 KB LDS (npx2 * max(N2, F3^2) <= 20480 floats)
+  static constexpr int kMaxPx = 20480 / (N2 > F3 * F3 ? N2 : F3 * F3);
+  static constexpr int kUnitsPerWave = ((kMaxPx + 15) / 16 + 7) / 8;
+  int region;  // one ping-pong region: max(A2 tile, Q of whole units, reduction scratch)
   int d3off;   // delta3 grid offset (F3-1) * (w2 + 1)
   int nd3;     // delta3 grid size (zero tail covers chunk overrun)
   __host__ __device__ L3Lds(int w2, int h2) {
     const int npx2 = w2 * h2, nch = (npx2 + 31) / 32;
     int r = npx2 * N2;
-    if (npx2 * F3 * F3 > r) r = npx2 * F3 * F3;
+    const int npad = (npx2 + 15) / 16 * 16;  // Q is written for whole 16-pixel units
+    if (npad * F3 * F3 > r) r = npad * F3 * F3;
     if (((N2 + 31) / 32) * 1024 > r) r = ((N2 + 31) / 32) * 1024;
     region = (r + 3) & ~3;
     d3off = (F3 - 1) * (w2 + 1);
@@ -92,6 +114,7 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
   constexpr int KQ = N2 / 4;          // Q k-steps (over channels)
   constexpr int NW3 = K3 * N2;        // gW3 size; slab row = NW3 + 1 (gB3)
   constexpr int NQ = N2 / 4;          // quads per A2 row
+  constexpr int kUMax = L3Lds<N2, F3>::kUnitsPerWave;  // unit slots per wave
   static_assert(K3 <= 32, "taps must fit two 16-wide MFMA tiles");
   static_assert(N2 % 16 == 0 && N2 <= 32 && (NQ & (NQ - 1)) == 0, "n2 must be 16 or 32");
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -122,7 +145,7 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
   auto tap_off = [&](int tap) { return tap < K3 ? (tap / F3) * g.w2 + tap % F3 : 0; };
   // B operand of Q: W3[tap = 16t + lq][c = 4s + lg]
   float wq[KQ][TT];
-  // B operand of delta2: W3[tap = 4s + lg][n = 16t + lq]
+  // A operand of delta2^T: W3[tap = 4s + lg][n = 16t + lq]
   float wd[KT][NT];
 #pragma unroll
   for (int s = 0; s < KQ; s++)
@@ -144,7 +167,7 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
   // pixels, so the A2 swizzle of a unit-relative pixel is unit independent):
   //  qz[s]:     Q A operand A2[u0 + lq][4s + lg]
   //  bsw[t][j]: A2[u0 + 4lg + s][16t + lq] for s >> 1 == j
-  //  od[s]:     delta3 window of tap 4s + lg (delta2 A operand, pixel u0 + lq)
+  //  od[s]:     delta3 window of tap 4s + lg (delta2^T B operand, pixel u0 + lq)
   //  goff[t]:   delta3 window of tap 16t + lq (gW3 A operand; lanes past the
   //             taps read a real window: their gW3 rows are discarded)
   int qz[KQ], bsw[NT][2], od[KT], goff[TT];
@@ -159,6 +182,10 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
   for (int s = 0; s < KT; s++) od[s] = d3off - tap_off(4 * s + lg);
 #pragma unroll
   for (int t = 0; t < TT; t++) goff[t] = d3off - tap_off(16 * t + lq);
+  //  mo[t]:     quad 4t + lg of A2 row u0 + lq (relu' mask of transposed delta2)
+  int mo[NT];
+#pragma unroll
+  for (int t = 0; t < NT; t++) mo[t] = lq * N2 + 4 * ((4 * t + lg) ^ ((lq >> 1) & (NQ - 1)));
 
   f32x4 gacc[TT][NT];
 #pragma unroll
@@ -199,6 +226,21 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
     }                                                                                  \
   } while (0)
 
+  // masked delta2 of this wave's units (slot j = unit wave + 8j), held
+  // until the next sample's Q phase; D2 rows past the sample are not stored
+  f32x4 d2k[kUMax][NT];
+  float* d2dst = D2;
+  bool d2pend = false;
+#define SRCNN_L3_D2_STORE(J)                                                           \
+  do {                                                                                 \
+    const int q_ = 16 * (wave + nwaves * (J)) + lq;                                    \
+    if (d2pend && q_ < npx2 && !kL3DiagNoStore) {                                      \
+      float* dst_ = d2dst + (size_t)q_ * N2 + 4 * lg;                                  \
+      _Pragma("unroll") for (int t = 0; t < NT; t++)                                   \
+        *reinterpret_cast<f32x4*>(dst_ + 16 * t) = d2k[J][t];                          \
+    }                                                                                  \
+  } while (0)
+
   int cur = 0;
   if ((int)blockIdx.x < g.batch) {
     SRCNN_L3_A2_DMA(blockIdx.x, smem);
@@ -223,38 +265,40 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
     const bool has_next = sample + (int)gridDim.x < g.batch;
     if (has_next) SRCNN_L3_T_PREFETCH(sample + gridDim.x);
 
-    // ---- Q = A2 . W3^T per 16-pixel unit (rows past npx2 are discarded) ----
-    for (int u = wave; u < nunit; u += nwaves) {
-      const int u0 = 16 * u;
-      const float* a2u = a2s + u0 * N2;
-      float av[KQ];
+    // ---- Q = A2 . W3^T per 16-pixel unit (rows past npx2 are discarded);
+    // the PREVIOUS sample's masked delta2 leaves to HBM under these MFMAs ----
 #pragma unroll
-      for (int s = 0; s < KQ; s++) av[s] = a2u[qz[s]];
-      __builtin_amdgcn_sched_barrier(0);  // all operand reads in flight before the MFMAs
-      f32x4 acc[TT];
+    for (int j = 0; j < kUMax; j++) {
+      const int u = wave + nwaves * j;
+      if (u < nunit) {
+        const int u0 = 16 * u;
+        const float* a2u = a2s + u0 * N2;
+        float av[KQ];
 #pragma unroll
-      for (int t = 0; t < TT; t++) acc[t] = mfma::zero4();
+        for (int s = 0; s < KQ; s++) av[s] = a2u[qz[s]];
+        __builtin_amdgcn_sched_barrier(0);  // all operand reads in flight before the MFMAs
+        f32x4 acc[TT];
 #pragma unroll
-      for (int s = 0; s < KQ; s++)
+        for (int t = 0; t < TT; t++) acc[t] = mfma::zero4();
 #pragma unroll
-        for (int t = 0; t < TT; t++) acc[t] = mfma::mma16(av[s], wq[s][t], acc[t]);
-      // Q[u0 + 4lg + i][tap = 16t + lq]
+        for (int s = 0; s < KQ; s++)
 #pragma unroll
-      for (int t = 0; t < TT; t++) {
-        const int tap = 16 * t + lq;
-        if (tap < K3) {
-          float* qd = qs + (u0 + 4 * lg) * K3 + tap;
-          if (u0 + 16 <= npx2) {
+          for (int t = 0; t < TT; t++) acc[t] = mfma::mma16(av[s], wq[s][t], acc[t]);
+        SRCNN_L3_D2_STORE(j);
+        // Q[u0 + 4lg + i][tap = 16t + lq] (the region holds whole units: rows
+        // past the sample are written too, never read)
+#pragma unroll
+        for (int t = 0; t < TT; t++) {
+          const int tap = 16 * t + lq;
+          if (tap < K3) {
+            float* qd = qs + (u0 + 4 * lg) * K3 + tap;
 #pragma unroll
             for (int i = 0; i < 4; i++) qd[i * K3] = acc[t][i];
-          } else {
-#pragma unroll
-            for (int i = 0; i < 4; i++)
-              if (u0 + 4 * lg + i < npx2) qd[i * K3] = acc[t][i];
           }
         }
       }
     }
+    d2pend = false;
     __syncthreads();
     SRCNN_L3_TICK(1);
 
@@ -282,39 +326,31 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
     SRCNN_L3_TICK(2);
 
     // Q is consumed: the next sample's A2 streams into its region meanwhile
+    // (Measured slower: loading the next A2 into registers under the Q MFMAs
+    // and writing it here, so its HBM reads leave the delta2 phase.)
+#ifndef SRCNN_L3_DIAG_NODMA
     if (has_next) SRCNN_L3_A2_DMA(sample + gridDim.x, other);
+#endif
 
-    // ---- per 16-pixel unit: delta2 and gW3 MFMAs; the delta2 epilogue
-    // (relu' mask + store) of the PREVIOUS unit is issued behind the current
-    // unit's MFMAs, so the matrix core never waits for it ----
+    // ---- per 16-pixel unit: delta2 and gW3 MFMAs ----
     //   delta2[q][n] = [A2 > 0] * sum_tap delta3(q - off(tap)) W3[tap][n]
     //   gW3[tap][n] += sum_p delta3(p - off(tap)) A2[p][n]
-    // gW3's pixel k-slot (s, lg) is pixel u0 + 4lg + s: its B operand
-    // A2[u0 + 4lg + s][16t + lq] is then also the relu' mask of delta2's C
-    // register s, so the epilogue reads nothing.  Rows past the sample: the
-    // d3g tail is zero (gW3) and their delta2 is not stored.
-    {
-      f32x4 prev[NT];
-      float pm[4][NT];
-      int pu0 = -1;  // first pixel of the unit whose delta2 is pending
-      float* d2s = D2 + (size_t)sample * npx2 * N2;
-#define SRCNN_L3_D2_EPILOGUE(U0, ACC, MASK)                                            \
-  do {                                                                                 \
-    float* dst_ = d2s + (size_t)((U0) + 4 * lg) * N2 + lq;                             \
-    if ((U0) + 16 <= npx2) {                                                           \
-      _Pragma("unroll") for (int i = 0; i < 4; i++)                                    \
-        _Pragma("unroll") for (int t = 0; t < NT; t++)                                 \
-          dst_[i * N2 + 16 * t] = (MASK)[i][t] > 0.0f ? (ACC)[t][i] : 0.0f;            \
-    } else {                                                                           \
-      _Pragma("unroll") for (int i = 0; i < 4; i++)                                    \
-        _Pragma("unroll") for (int t = 0; t < NT; t++)                                 \
-          if ((U0) + 4 * lg + i < npx2)                                                \
-            dst_[i * N2 + 16 * t] = (MASK)[i][t] > 0.0f ? (ACC)[t][i] : 0.0f;          \
-    }                                                                                  \
-  } while (0)
-      for (int u = wave; u < nunit; u += nwaves) {
+    // delta2 runs TRANSPOSED (M = channels, N = pixels): C register i of lane
+    // (lq, lg) in tile t is delta2[u0 + lq][16t + 4lg + i], four consecutive
+    // channels of one pixel, so a unit leaves as NT 16-B stores per lane; its
+    // relu' mask is one 16-B read of the same quad of the A2 image.
+    //
+    // The masked delta2 stays in registers (d2k) and is stored under the NEXT
+    // sample's Q MFMAs: this phase already streams the next A2 tile in by DMA,
+    // and with the stores here too it ran at the per-CU HBM rate (ablation:
+    // the stores were half of the phase) while the Q phase moved no bytes.
+#pragma unroll
+    for (int j = 0; j < kUMax; j++) {
+      const int u = wave + nwaves * j;
+      if (u < nunit) {
         const int u0 = 16 * u;
         float ad[KT], ag[4][TT], bg[4][NT];
+        f32x4 mk[NT];
         const float* dcu = d3g + u0 + lq;
 #pragma unroll
         for (int s = 0; s < KT; s++) ad[s] = dcu[od[s]];
@@ -327,6 +363,8 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
 #pragma unroll
           for (int t = 0; t < NT; t++) bg[s][t] = a2u[bsw[t][s >> 1] + s * N2];
         }
+#pragma unroll
+        for (int t = 0; t < NT; t++) mk[t] = *reinterpret_cast<const f32x4*>(a2s + u0 * N2 + mo[t]);
         __builtin_amdgcn_sched_barrier(0);  // all operand reads in flight before the MFMAs
         f32x4 acc[NT];
 #pragma unroll
@@ -334,29 +372,29 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
 #pragma unroll
         for (int s = 0; s < KT; s++)
 #pragma unroll
-          for (int t = 0; t < NT; t++) acc[t] = mfma::mma16(ad[s], wd[s][t], acc[t]);
+          for (int t = 0; t < NT; t++)
+            if (!kL3DiagNoD2) acc[t] = mfma::mma16(wd[s][t], ad[s], acc[t]);
 #pragma unroll
-        for (int s = 0; s < 4; s++)
+        for (int s = 0; s < 4 * !kL3DiagNoGW3; s++)
 #pragma unroll
           for (int t3 = 0; t3 < TT; t3++)
 #pragma unroll
             for (int t = 0; t < NT; t++)
               gacc[t3][t] = mfma::mma16(ag[s][t3], bg[s][t], gacc[t3][t]);
-        if (pu0 >= 0) SRCNN_L3_D2_EPILOGUE(pu0, prev, pm);
 #pragma unroll
-        for (int t = 0; t < NT; t++) {
-          prev[t] = acc[t];
+        for (int t = 0; t < NT; t++)
 #pragma unroll
-          for (int s = 0; s < 4; s++) pm[s][t] = bg[s][t];
-        }
-        pu0 = u0;
+          for (int i = 0; i < 4; i++) d2k[j][t][i] = mk[t][i] > 0.0f ? acc[t][i] : 0.0f;
       }
-      if (pu0 >= 0) SRCNN_L3_D2_EPILOGUE(pu0, prev, pm);
-#undef SRCNN_L3_D2_EPILOGUE
     }
+    d2dst = D2 + (size_t)sample * npx2 * N2;
+    d2pend = true;
     SRCNN_L3_TICK(3);
     cur ^= 1;
   }
+#pragma unroll
+  for (int j = 0; j < kUMax; j++) SRCNN_L3_D2_STORE(j);
+#undef SRCNN_L3_D2_STORE
 #undef SRCNN_L3_A2_DMA
 #undef SRCNN_L3_T_PREFETCH
 

@@ -74,6 +74,10 @@ struct Geom {
 #ifndef SRCNN_L12_GRID
 #define SRCNN_L12_GRID 1024  // grid cap (blocks), a multiple of 256 CUs x blocks per CU
 #endif
+#ifndef SRCNN_L12_PD
+#define SRCNN_L12_PD 4  // L1 X-gather prefetch distance (k-steps); 0 = compiler schedule
+#endif
+constexpr int kL12PD = SRCNN_L12_PD;
 #ifndef SRCNN_L12_WAVES
 #define SRCNN_L12_WAVES 2  // minimum waves per SIMD (register budget 512 / this)
 #endif
@@ -190,12 +194,24 @@ __global__ __launch_bounds__(256, SRCNN_L12_WAVES) void l12_fwd_kernel(
 #pragma unroll
       for (int t = 0; t < NT1; t++) acc1[t] = zero16();
       constexpr int kStoreEvery = (KS1 - 1) / NST;
-#pragma unroll
-      for (int s = 0; s < KS1; s++) {
+      // B operand of k-step s (tap K1 = the bias slot)
+      auto xg = [&](int s) {
         const int k0 = 2 * s;
         const int o0 = (k0 / F1) * kL12S + (k0 % F1);
-        float xv = xs[((k0 % F1) + 1 < F1 ? xbA : xbB) + o0];
-        if (s == KS1 - 1) xv = h ? 1.0f : xv;  // tap K1 = the bias slot
+        const float v = xs[((k0 % F1) + 1 < F1 ? xbA : xbB) + o0];
+        return s == KS1 - 1 ? (h ? 1.0f : v) : v;
+      };
+      // gathers run kL12PD k-steps ahead of their MFMAs, pinned by sched
+      // barriers: left alone, the scheduler issues each one just before its
+      // MFMA pair and the wave waits out the full LDS latency every step
+      float xq[KS1];
+#pragma unroll
+      for (int s = 0; s < kL12PD && s < KS1; s++) xq[s] = xg(s);
+#pragma unroll
+      for (int s = 0; s < KS1; s++) {
+        if (s + kL12PD < KS1) xq[s + kL12PD] = xg(s + kL12PD);
+        if (kL12PD > 0) __builtin_amdgcn_sched_barrier(0);
+        const float xv = kL12PD > 0 ? xq[s] : xg(s);
 #pragma unroll
         for (int t = 0; t < NT1; t++) acc1[t] = mma(SRCNN_W1F(s, t), xv, acc1[t]);
         if (s % kStoreEvery == kStoreEvery - 1 && s / kStoreEvery < NST) store_prev(s / kStoreEvery);
@@ -709,6 +725,7 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   if ((int)(w * h) > kXsMax || (int)w > kL12S || (int)h > kL12Rows || w3 <= 0 || h3 <= 0) return 0;
   const size_t lds3 = l3_lds_bytes<N2, F3>(ow, oh);
   if (lds3 > 160 * 1024 || w3 * h3 > kL3MaxOut) return 0;
+  if (((ow * oh + 15) / 16 + kL3Threads / 64 - 1) / (kL3Threads / 64) > L3Lds<N2, F3>::kUnitsPerWave) return 0;
   const int g12 = grid_for_batch(batch, SRCNN_L12_GRID);
   const int g3 = grid_for_batch(batch, 256);
   const int gd = grid_for_batch(batch, 512);
