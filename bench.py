@@ -34,6 +34,7 @@ import torch.distributed as dist  # noqa: E402
 
 PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA peak
 PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+NOMINAL_CLOCK_GHZ = 2.4    # MI355X_MICROARCH.md: max clock, the clock PEAK_FP32_TFLOPS assumes
 RIDGE = PEAK_FP32_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9)
 
 DEFAULT_NET = (64, 32, 9, 1, 5)
@@ -109,6 +110,26 @@ def kernel_work(name, work, net, w, h):
     flops = sum(work[s][0] for s in stages)
     nbytes = fused_bytes(net, w, h).get(name, sum(work[s][1] for s in stages))
     return flops, nbytes
+
+
+def held_clock(S, name):
+    """Shader clock (GHz) the chip held during the last launch of `name`
+    (in-kernel s_memtime / s_memrealtime probe, srcnn_profile_clock), or None."""
+    try:
+        return S.profile_clock(name)
+    except Exception:
+        return None
+
+
+def add_clock(out, ghz):
+    """Beside the nominal-clock fraction: the same achieved rate against the
+    peak scaled to the clock the chip held (MI355X_MICROARCH.md DVFS)."""
+    if out is None or not ghz:
+        return out
+    out["held_clock_ghz"] = round(ghz, 3)
+    if out["bound"] == "mfma":
+        out["frac_at_held_clock"] = round(out["frac"] * NOMINAL_CLOCK_GHZ / ghz, 4)
+    return out
 
 
 def roofline_of(name, launches_per_step, ms_per_step, work, tiles, pmc=None, net=DEFAULT_NET,
@@ -233,11 +254,16 @@ def forward_4k(S, net_t, frames=5, warmup=2, w=3840, h=2160):
     flops = 2.0 * (w1 * h1 * n1 * f1 * f1 + w2 * h2 * n2 * n1 * f2 * f2 + w3 * h3 * n2 * f3 * f3)
     kernels = {k: {"launches_per_frame": c / frames, "ms_per_frame": round(t / frames, 4)}
                for k, (c, t) in stats.items()}
-    return {"frame": "%dx%d" % (w, h), "frames": frames, "ms_per_frame": round(ms, 4),
-            "mpix_s": round(w * h / (ms * 1e-3) / 1e6, 1),
-            "tflops": round(flops / (ms * 1e-3) / 1e12, 2),
-            "roofline_frac": round(flops / (ms * 1e-3) / 1e12 / PEAK_FP32_TFLOPS, 4),
-            "algorithmic_gflop_per_frame": round(flops / 1e9, 2), "kernels": kernels}
+    res = {"frame": "%dx%d" % (w, h), "frames": frames, "ms_per_frame": round(ms, 4),
+           "mpix_s": round(w * h / (ms * 1e-3) / 1e6, 1),
+           "tflops": round(flops / (ms * 1e-3) / 1e12, 2),
+           "roofline_frac": round(flops / (ms * 1e-3) / 1e12 / PEAK_FP32_TFLOPS, 4),
+           "algorithmic_gflop_per_frame": round(flops / 1e9, 2), "kernels": kernels}
+    ghz = held_clock(S, "fwd_l123_mfma")
+    if ghz:
+        res["held_clock_ghz"] = round(ghz, 3)
+        res["roofline_frac_at_held_clock"] = round(res["roofline_frac"] * NOMINAL_CLOCK_GHZ / ghz, 4)
+    return res
 
 
 WIDE_NET = (128, 64, 9, 5, 5)
@@ -385,7 +411,8 @@ def main():
         roof = None
         if dominant:
             cnt, ms = stats[dominant]
-            roof = roofline_of(dominant, cnt / K, ms / K, work, B, pmc)
+            roof = add_clock(roofline_of(dominant, cnt / K, ms / K, work, B, pmc),
+                             held_clock(S, dominant))
         # whole-step roofline: T_roof = sum_stage max(F/peak, B/peak)
         t_roof = sum(max(f / (PEAK_FP32_TFLOPS * 1e12), b / (PEAK_HBM_GBS * 1e9))
                      for f, b in work.values()) * B

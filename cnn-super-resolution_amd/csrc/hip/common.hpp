@@ -60,6 +60,45 @@ struct Scope {
 // bracket the launches that follow in this scope for the profiler
 #define SRCNN_PROFILE(name, stream) ::srcnn::prof::Scope srcnn_prof_scope_(name, stream)
 
+// Held-clock probe (MI355X_MICROARCH.md "DVFS give-back", item 6): the first
+// kClockBlocks blocks of a fused kernel record the s_memtime (shader clock)
+// and s_memrealtime (100 MHz) deltas over their lifetime into a per-kernel
+// slot of a device array; srcnn_profile_clock() reports their median ratio.
+// Two scalar counter reads per wave and one 16-B vector store per block.
+namespace srcnn {
+constexpr int kClockBlocks = 8;
+}
+#define SRCNN_CLOCK_BEGIN()                                                        \
+  const unsigned long long srcnn_clk_c0_ = __builtin_amdgcn_s_memtime();           \
+  const unsigned long long srcnn_clk_r0_ = __builtin_amdgcn_s_memrealtime()
+#define SRCNN_CLOCK_END(ARR, SLOT)                                                 \
+  do {                                                                             \
+    if (blockIdx.x < (unsigned)::srcnn::kClockBlocks && threadIdx.x == 0) {        \
+      const unsigned long long c1_ = __builtin_amdgcn_s_memtime();                 \
+      const unsigned long long r1_ = __builtin_amdgcn_s_memrealtime();             \
+      (ARR)[SLOT][blockIdx.x][0] = c1_ - srcnn_clk_c0_;                            \
+      (ARR)[SLOT][blockIdx.x][1] = r1_ - srcnn_clk_r0_;                            \
+    }                                                                              \
+  } while (0)
+
+namespace srcnn {
+// median shader clock (GHz) over the probe blocks of one slot; -1 if unset
+inline double clock_ghz(const unsigned long long (*a)[2]) {
+  double v[kClockBlocks];
+  int n = 0;
+  for (int b = 0; b < kClockBlocks; b++)
+    if (a[b][1] > 0) v[n++] = (double)a[b][0] / (double)a[b][1] * 0.1;
+  if (n == 0) return -1.0;
+  for (int i = 1; i < n; i++)
+    for (int j = i; j > 0 && v[j - 1] > v[j]; j--) {
+      const double t = v[j];
+      v[j] = v[j - 1];
+      v[j - 1] = t;
+    }
+  return n % 2 ? v[n / 2] : 0.5 * (v[n / 2 - 1] + v[n / 2]);
+}
+}  // namespace srcnn
+
 #define SRCNN_REQUIRE(cond, ...)                                                   \
   do {                                                                             \
     if (!(cond)) return ::srcnn::fail(SRCNN_ERR_INVALID, __VA_ARGS__);             \

@@ -32,6 +32,9 @@ using mfma::f32x16;
 using mfma::mma;
 using mfma::zero16;
 
+// held-clock probe slot (common.hpp) of fwd_l123
+__device__ unsigned long long g_clk_fwd[1][kClockBlocks][2];
+
 namespace {
 
 constexpr int kFwdRW = 32;        // region width (one chunk per region row)
@@ -75,6 +78,7 @@ __global__ __launch_bounds__(256, SRCNN_FWD_WAVES) void fwd_l123_kernel(
   __shared__ __attribute__((aligned(16))) float qs[4][32][QS];  // per-wave Q[pixel][tap]
   __shared__ float accs[F3][EHM][EW];  // [dy][partial row][partial col]
 
+  SRCNN_CLOCK_BEGIN();
   const int lane = mfma::lane_id(), wave = mfma::wave_id();
   const int h = lane >> 5, li = lane & 31;
   const int EH = g.rh + F3 - 1;
@@ -224,6 +228,7 @@ __global__ __launch_bounds__(256, SRCNN_FWD_WAVES) void fwd_l123_kernel(
       dst[i] = v;
     }
   }
+  SRCNN_CLOCK_END(g_clk_fwd, 0);
 }
 
 // A3[y][x] = B3 + the partials of the regions (ry, rx) in {y, y+f3-1}/rh x
@@ -300,6 +305,13 @@ int run_forward(const float* X, uint32_t w, uint32_t h, uint32_t batch, const fl
 }
 
 }  // namespace
+
+int forward_clock(double* ghz) {
+  unsigned long long a[1][kClockBlocks][2];
+  SRCNN_HIP_TRY(hipMemcpyFromSymbol(a, HIP_SYMBOL(g_clk_fwd), sizeof(a)));
+  *ghz = clock_ghz(a[0]);
+  return SRCNN_OK;
+}
 
 int forward(const srcnn_net* net, const float* X, uint32_t w, uint32_t h, uint32_t batch,
             const float* params, float* out, void* ws, size_t ws_bytes, hipStream_t s,

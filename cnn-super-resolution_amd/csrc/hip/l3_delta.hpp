@@ -117,6 +117,7 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
   constexpr int kUMax = L3Lds<N2, F3>::kUnitsPerWave;  // unit slots per wave
   static_assert(K3 <= 32, "taps must fit two 16-wide MFMA tiles");
   static_assert(N2 % 16 == 0 && N2 <= 32 && (NQ & (NQ - 1)) == 0, "n2 must be 16 or 32");
+  SRCNN_CLOCK_BEGIN();
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int npx2 = g.w2 * g.h2;
   const int nunit = (npx2 + 15) / 16;
@@ -396,6 +397,7 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
   for (int j = 0; j < kUMax; j++) SRCNN_L3_D2_STORE(j);
 #undef SRCNN_L3_D2_STORE
 #undef SRCNN_L3_A2_DMA
+  SRCNN_CLOCK_END(g_clk, 1);
 #undef SRCNN_L3_T_PREFETCH
 
 #ifdef SRCNN_L3_TIMING

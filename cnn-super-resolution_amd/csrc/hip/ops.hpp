@@ -60,6 +60,9 @@ struct SlabSeg {
   int nslab, P;
 };
 int reduce_slabs(const SlabSeg* segs, int nseg, hipStream_t s);
+// held-clock probes (common.hpp): slot 0 l12_fwd, 1 l3_delta, 2 d1_grad12
+int train_clock(int slot, double* ghz);
+int forward_clock(double* ghz);
 }  // namespace fused
 
 // Training step for nets with a spatial middle layer (train_wide.hip), e.g.

@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "common.hpp"
+#include "ops.hpp"
 
 namespace srcnn {
 
@@ -158,6 +159,15 @@ int srcnn_profile_print(void) {
   }
   fflush(stdout);
   return SRCNN_OK;
+}
+
+int srcnn_profile_clock(const char* kernel, double* ghz) {
+  SRCNN_REQUIRE(kernel && ghz, "srcnn_profile_clock: null argument");
+  static const char* const kTrain[] = {"l12_fwd_mfma", "l3_delta_fused", "delta1_grad12_fused"};
+  for (int i = 0; i < 3; i++)
+    if (!strcmp(kernel, kTrain[i])) return srcnn::fused::train_clock(i, ghz);
+  if (!strcmp(kernel, "fwd_l123_mfma")) return srcnn::fused::forward_clock(ghz);
+  return srcnn::fail(SRCNN_ERR_INVALID, "srcnn_profile_clock: no clock probe in kernel '%s'", kernel);
 }
 
 int srcnn_device_count(int* count) {

@@ -68,6 +68,9 @@ struct Geom {
 //         mfma.hpp), A = W2 (registers); one extra MFMA adds B2
 // so L2 needs no LDS transpose at all, and each lane ends with consecutive
 // channels of ONE pixel: A1 / A2 leave as 16-B stores straight from registers.
+// held-clock probe slots (common.hpp): 0 l12_fwd, 1 l3_delta, 2 d1_grad12
+__device__ unsigned long long g_clk[3][kClockBlocks][2];
+
 #ifndef SRCNN_L12_W1LDS
 #define SRCNN_L12_W1LDS 0
 #endif
@@ -91,6 +94,7 @@ __global__ __launch_bounds__(256, SRCNN_L12_WAVES) void l12_fwd_kernel(
                 "transposed l12: one 32-row L2 tile, odd tap count");
   __shared__ float xs[kL12Tile];  // X tile at the fixed row stride kL12S (+ zero rows)
 
+  SRCNN_CLOCK_BEGIN();
   const int lane = mfma::lane_id(), wave = mfma::wave_id();
   const int h = lane >> 5, li = lane & 31;
   const int npx = g.ow * g.oh;
@@ -240,6 +244,7 @@ __global__ __launch_bounds__(256, SRCNN_L12_WAVES) void l12_fwd_kernel(
     for (int k = 0; k < NST; k++) store_prev(k);
     pok = false;
   }
+  SRCNN_CLOCK_END(g_clk, 0);
 }
 #undef SRCNN_W1F
 
@@ -247,7 +252,9 @@ __global__ __launch_bounds__(256, SRCNN_L12_WAVES) void l12_fwd_kernel(
 
 #ifdef SRCNN_D1_TIMING
 // diagnostics build only: wave 0's cycles per section of the chunk loop
-__device__ unsigned long long g_d1_timing[1024][6];
+// [block][wave][section]; [6], [7]: s_memtime / s_memrealtime (100 MHz) deltas
+// over the block, whose ratio is the shader clock the chip held
+__device__ unsigned long long g_d1_timing[1024][4][8];
 #define SRCNN_D1_TICK(PH)                           \
   do {                                              \
     const unsigned long long now_ = clock64();      \
@@ -277,6 +284,10 @@ __device__ unsigned long long g_d1_timing[1024][6];
 // With f1 = 9 that is 80 MFMA taps + 1 VALU tap, where a 32-row tap tiling
 // issues 96 rows (81 taps + ones row + 14 pad): 1/6 fewer gW1 MFMA cycles.
 // ---------------------------------------------------------------------------
+#ifndef SRCNN_D1_TOPWAIT
+#define SRCNN_D1_TOPWAIT 1  // sample top waits for the X tile only, not the next chunk's operands
+#endif
+constexpr bool kD1TopWait = SRCNN_D1_TOPWAIT;
 template <int N1, int N2, int F1>
 __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
     const float* __restrict__ X, const float* __restrict__ A1, const float* __restrict__ D2,
@@ -307,6 +318,7 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
   float* w2s = xsb + 2 * kXsMax;       // [N1][WS]: W2[c][n]
   float* d2w = w2s + N1 * WS;          // [4][32][DS]
 
+  SRCNN_CLOCK_BEGIN();
   const int lane = mfma::lane_id(), wave = mfma::wave_id();
   const int h = lane >> 5, li = lane & 31;
   const int lq = lane & 15, lg = lane >> 4;  // 16x16x4 operand row / k group
@@ -391,6 +403,7 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
 
 #ifdef SRCNN_D1_TIMING
   unsigned long long tacc[6] = {0, 0, 0, 0, 0, 0}, tlast = clock64();
+  const unsigned long long c0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
 #endif
   // X tile of a sample -> xs buffer by 4-byte LDS-DMA (lane-linear)
   const int xn = g.W * g.H, xk = (xn + 63) / 64;
@@ -416,9 +429,22 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
   int xbuf = 0;
   for (int sample = blockIdx.x; sample < g.batch; sample += gridDim.x, xbuf ^= 1) {
     // this sample's X tile (every wave's share) has landed; the previous
-    // sample's readers of the other X buffer are done
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    // sample's readers of the other X buffer are done.  A wave with chunks
+    // issued its share of this X tile before at least kDmaK operand DMAs
+    // (those of its next chunk are the most recent), so vmcnt(kDmaK) is
+    // enough: the next chunk's operands need not land before the barrier.
+    // (__syncthreads() would add its own vmcnt(0): a bare s_barrier after
+    // explicit waits; lgkmcnt(0) retires this wave's X reads of the buffer
+    // the others are about to refill)
+    if (!kD1TopWait || wave >= nch) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    } else {
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(kD1TopWait ? kDmaK : 0) : "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+    SRCNN_D1_TICK(4);
     const float* xs = xsb + xbuf * kXsMax;
     const int next = sample + (int)gridDim.x;
     const bool has_next = next < g.batch;
@@ -443,6 +469,8 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
       for (int pm = 0; pm < 2; pm++)
 #pragma unroll
         for (int t = 0; t < NQ; t++) d1[pm][t] = mfma::zero4();
+      // (Measured slower: these operands read one delta1/gW2 super-step ahead
+      // into two register sets pinned by sched barriers -- 3 VGPR spills.)
 #pragma unroll
       for (int s = 0; s < KD; s++) {
         const int n = 4 * s + lg;
@@ -560,9 +588,14 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
 #undef SRCNN_D1_X_DMA
 
 #ifdef SRCNN_D1_TIMING
-  if (lane == 0 && wave == 0)
-    for (int k = 0; k < 6; k++) g_d1_timing[blockIdx.x][k] = tacc[k];
+  if (lane == 0) {
+    const unsigned long long c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    for (int k = 0; k < 6; k++) g_d1_timing[blockIdx.x][wave][k] = tacc[k];
+    g_d1_timing[blockIdx.x][wave][6] = c1 - c0;
+    g_d1_timing[blockIdx.x][wave][7] = r1 - r0;
+  }
 #endif
+  SRCNN_CLOCK_END(g_clk, 2);
   // ---- block reduction (waves in order) into LDS, then one slab per block ----
   __syncthreads();
   float* red = smem;
@@ -787,6 +820,13 @@ static int dispatch_one(const srcnn_net* net, const float* X, const float* T, ui
     return 0;
   return run<N1, N2, F1, F3>(X, T, w, h, batch, params, grads, sq_err, A1, A2, D2, slab,
                              slab_bytes, s, query_only, need);
+}
+
+int train_clock(int slot, double* ghz) {
+  unsigned long long a[3][kClockBlocks][2];
+  SRCNN_HIP_TRY(hipMemcpyFromSymbol(a, HIP_SYMBOL(g_clk), sizeof(a)));
+  *ghz = clock_ghz(a[slot]);
+  return SRCNN_OK;
 }
 
 int train_fwd_bwd(const srcnn_net* net, const float* X, const float* T, uint32_t w, uint32_t h,

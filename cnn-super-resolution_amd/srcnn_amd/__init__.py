@@ -91,6 +91,7 @@ SIGNATURES = {
     "srcnn_profile_get": (_I, [_I, ctypes.c_char_p, _S, ctypes.POINTER(ctypes.c_uint64),
                                ctypes.POINTER(ctypes.c_double)]),
     "srcnn_profile_print": (_I, []),
+    "srcnn_profile_clock": (_I, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double)]),
     "srcnn_set_path": (_I, [_I]),
     "srcnn_get_path": (_I, []),
 }
@@ -343,6 +344,13 @@ def profile_stats():
         _call("srcnn_profile_get", i, buf, 256, ctypes.byref(cnt), ctypes.byref(ms))
         out[buf.value.decode()] = (cnt.value, ms.value)
     return out
+
+
+def profile_clock(kernel):
+    """Shader clock (GHz) held during the last launch of a fused kernel, or None."""
+    ghz = ctypes.c_double()
+    _call("srcnn_profile_clock", kernel.encode(), ctypes.byref(ghz))
+    return ghz.value if ghz.value > 0 else None
 
 
 def profile_print():

@@ -213,6 +213,13 @@ SRCNN_API int srcnn_profile_get(int index, char* name, size_t name_len,
                                 uint64_t* launches, double* total_ms);
 /* prints "Kernel '<name>' total execution time: <ns>ns = <s>s" per kernel */
 SRCNN_API int srcnn_profile_print(void);
+/* Shader clock (GHz) the chip held during the most recent launch of a fused
+ * kernel ("l12_fwd_mfma", "l3_delta_fused", "delta1_grad12_fused",
+ * "fwd_l123_mfma"): median over the kernel's first 8 workgroups of the
+ * s_memtime / s_memrealtime (100 MHz) deltas they record in-kernel
+ * (MI355X DVFS under MFMA load).  *ghz = -1 when the kernel has not run.
+ * An MI355X extension; the reference has no counterpart.  Synchronous. */
+SRCNN_API int srcnn_profile_clock(const char* kernel, double* ghz);
 
 /* Kernel-path selection (for A/B measurement and parity tests):
  * 0 = auto (fast specialisations where the shape matches), 1 = generic only. */

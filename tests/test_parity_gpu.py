@@ -443,6 +443,28 @@ def test_full_batch_gradients_vs_oracle(S):
     assert_close(H(g3), got, RTOL, "chunked accumulation")
 
 
+def test_held_clock_probe(S):
+    """srcnn_profile_clock: the in-kernel s_memtime / s_memrealtime probe of the
+    fused kernels reports a plausible shader clock after a launch (MI355X max
+    2.4 GHz; under MFMA load the chip holds less), and rejects other names."""
+    cfg = NETS["default"]
+    net = S.Net(*cfg)
+    batch, size = 512, 33
+    rng = np.random.default_rng(7)
+    X, T = make_batch(rng, batch, size, size)
+    params = make_params(rng, cfg, sd=0.05)
+    nbytes = S.train_workspace_bytes(net, size, size, batch)
+    ws = torch.empty(nbytes // 4 + 64, dtype=torch.float32, device="cuda")
+    g = zeros(params.size)
+    S.train_fwd_bwd(net, D(X), D(T), size, size, batch, D(params), g, None, ws, nbytes)
+    torch.cuda.synchronize()
+    for k in ("l12_fwd_mfma", "l3_delta_fused", "delta1_grad12_fused"):
+        ghz = S.profile_clock(k)
+        assert ghz is not None and 0.3 < ghz < 3.0, (k, ghz)
+    with pytest.raises(S.SrcnnError):
+        S.profile_clock("no_such_kernel")
+
+
 # ----------------------------------------------------------------------------
 # error behaviour (reference: std::runtime_error from the launchers)
 # ----------------------------------------------------------------------------

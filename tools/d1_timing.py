@@ -8,7 +8,7 @@ import sys
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["SRCNN_HIP_LIB"] = os.path.join(ROOT, "cnn-super-resolution_amd/lib/variants/libsrcnn_hip_d1t.so")
+os.environ.setdefault("SRCNN_HIP_LIB", os.path.join(ROOT, "cnn-super-resolution_amd/lib/variants/libsrcnn_hip_d1t.so"))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "cnn-super-resolution_amd"), os.path.join(ROOT, "tests")]
 import torch  # noqa: E402
 import srcnn_amd as S  # noqa: E402
@@ -27,11 +27,22 @@ ws = torch.empty(nb // 4 + 64, device=dev)
 for _ in range(3):
     S.train_fwd_bwd(net, Xd, Td, 33, 33, B, p, g, None, ws, nb)
 torch.cuda.synchronize()
-buf = (ctypes.c_ulonglong * (1024 * 6))()
+buf = (ctypes.c_ulonglong * (1024 * 4 * 8))()
 assert S.lib().srcnn_debug_d1_timing(buf) == 0
-t = np.array(buf, dtype=np.float64).reshape(1024, 6)[:512]
-names = ["wait DMA (+xbt)", "delta1", "gW2", "issue DMA", "gW1", "other (sample top, X tile)"]
-tot = t.sum(axis=1).mean()
-for i, n in enumerate(names):
-    print("%-18s %10.0f cycles/block  %5.1f%%  (%.0f per chunk)" % (n, t[:, i].mean(), 100 * t[:, i].mean() / tot, t[:, i].mean() / 40))
-print("total %.0f cycles/block = %.1f us at 2.2 GHz" % (tot, tot / 2.2e3))
+t8 = np.array(buf, dtype=np.float64).reshape(1024, 4, 8)
+t8 = t8[t8[:, :, :6].sum(axis=(1, 2)) > 0]
+clk = t8[:, :, 6] / np.maximum(t8[:, :, 7], 1) * 0.1  # GHz (s_memrealtime ticks at 100 MHz)
+print("held shader clock over the kernel: median %.3f GHz (min %.3f, max %.3f); block span %.1f us"
+      % (np.median(clk), clk.min(), clk.max(), np.median(t8[:, :, 7]) / 100.0))
+t = t8[:, :, :6]
+nb = len(t)
+chunks = (B / nb) * 20 / 4  # chunks per wave (20 per 33x33 sample)
+# NOTE: the compiler does not order s_memtime against MFMAs: the section
+# split is approximate (e.g. "other" absorbs gW1 MFMAs issued after its tick)
+names = ["wait DMA (+xbt)", "delta1", "gW2", "sample top (vmcnt+barrier)", "gW1", "other"]
+for w in range(4):
+    tot = t[:, w].sum(axis=1).mean()
+    print("wave %d: total %.0f cycles/block = %.1f us at 2.2 GHz" % (w, tot, tot / 2.2e3))
+    for i, n in enumerate(names):
+        print("   %-28s %10.0f cycles/block  %5.1f%%  (%.0f per chunk)" % (n, t[:, w, i].mean(), 100 * t[:, w, i].mean() / tot, t[:, w, i].mean() / chunks))
+print("product probe (srcnn_profile_clock, blocks 0-7): %.3f GHz" % S.profile_clock("delta1_grad12_fused"))
