@@ -284,6 +284,14 @@ __device__ unsigned long long g_d1_timing[1024][4][8];
 // With f1 = 9 that is 80 MFMA taps + 1 VALU tap, where a 32-row tap tiling
 // issues 96 rows (81 taps + ones row + 14 pad): 1/6 fewer gW1 MFMA cycles.
 // ---------------------------------------------------------------------------
+// diagnostics builds only (results invalid): drop one part of the d1 chunk
+#ifdef SRCNN_D1_DIAG
+constexpr int kD1Diag = SRCNN_D1_DIAG;
+#else
+constexpr int kD1Diag = 0;
+#endif
+constexpr bool kD1DiagNoD1 = kD1Diag & 1, kD1DiagNoGW2 = kD1Diag & 2, kD1DiagNoMask = kD1Diag & 4,
+               kD1DiagNoGW1 = kD1Diag & 8, kD1DiagNoDma = kD1Diag & 16;
 #ifndef SRCNN_D1_TOPWAIT
 #define SRCNN_D1_TOPWAIT 1  // sample top waits for the X tile only, not the next chunk's operands
 #endif
@@ -482,7 +490,8 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
 #pragma unroll
         for (int pm = 0; pm < 2; pm++)
 #pragma unroll
-          for (int t = 0; t < NQ; t++) d1[pm][t] = mfma::mma16(a[pm], b[t], d1[pm][t]);
+          for (int t = 0; t < NQ; t++)
+            if (!kD1DiagNoD1) d1[pm][t] = mfma::mma16(a[pm], b[t], d1[pm][t]);
       }
       SRCNN_D1_TICK(2);
       // gW2[c][n] += sum_p A1[p][c] delta2[p][n]; gB2[n] += sum_p delta2[p][n]
@@ -495,7 +504,8 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
           const float b = n < N2 ? d2me[pr * DS + n] : 0.0f;
           gb2[u] += b;
 #pragma unroll
-          for (int t = 0; t < NT1; t++) g2[t][u] = mma(a1me[pr * A1P + 32 * t + li], b, g2[t][u]);
+          for (int t = 0; t < NT1; t++)
+            if (!kD1DiagNoGW2) g2[t][u] = mma(a1me[pr * A1P + 32 * t + li], b, g2[t][u]);
         }
       }
 
@@ -507,7 +517,8 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
         for (int t = 0; t < NQ; t++)
 #pragma unroll
           for (int i = 0; i < 4; i++)
-            d1[pm][t][i] = a1me[(16 * pm + 4 * lg + i) * A1P + 16 * t + lq] > 0.0f ? d1[pm][t][i] : 0.0f;
+            if (!kD1DiagNoMask)
+              d1[pm][t][i] = a1me[(16 * pm + 4 * lg + i) * A1P + 16 * t + lq] > 0.0f ? d1[pm][t][i] : 0.0f;
 
       SRCNN_D1_TICK(3);
       // next chunk's operand DMA overlaps the gW1 MFMAs (the images' reads retired)
@@ -560,7 +571,8 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
 #pragma unroll
           for (int m = 0; m < MT; m++)
 #pragma unroll
-            for (int t = 0; t < NQ; t++) g1[m][t] = mfma::mma16(acur[m], d1[pm][t][i], g1[m][t]);
+            for (int t = 0; t < NQ; t++)
+              if (!kD1DiagNoGW1) g1[m][t] = mfma::mma16(acur[m], d1[pm][t][i], g1[m][t]);
 #pragma unroll
           for (int t = 0; t < NQ; t++) {
 #pragma unroll
@@ -569,7 +581,7 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
           }
 #pragma unroll
           for (int k = 0; k < kDmaPerStep; k++)
-            if (kDmaPerStep * s + k < kDmaK) SRCNN_D1_DMA_K(dsmp, dch, kDmaPerStep * s + k);
+            if (kDmaPerStep * s + k < kDmaK && !kD1DiagNoDma) SRCNN_D1_DMA_K(dsmp, dch, kDmaPerStep * s + k);
           if (s + 1 < 8) {
 #pragma unroll
             for (int m = 0; m < MT; m++) acur[m] = anxt[m];
