@@ -27,6 +27,8 @@ int check_layer(const char* who, uint32_t n_prev, uint32_t n_cur, uint32_t f) {
 struct NetDims {
   uint32_t w1, h1, w2, h2, w3, h3;
   size_t s1, s2, s3;  // per-sample floats of A1, A2, A3
+  size_t s1p;         // A1 region per sample: whole 32-pixel chunks (the fused
+                      // step stores A1 blocked per chunk, train_fused.hip)
 };
 
 int net_dims(const srcnn_net* net, uint32_t w, uint32_t h, NetDims* d) {
@@ -45,6 +47,7 @@ int net_dims(const srcnn_net* net, uint32_t w, uint32_t h, NetDims* d) {
   d->w3 = d->w2 - net->f3 + 1;
   d->h3 = d->h2 - net->f3 + 1;
   d->s1 = (size_t)d->w1 * d->h1 * net->n1;
+  d->s1p = ((size_t)d->w1 * d->h1 + 31) / 32 * 32 * net->n1;
   d->s2 = (size_t)d->w2 * d->h2 * net->n2;
   d->s3 = (size_t)d->w3 * d->h3;
   return SRCNN_OK;
@@ -230,7 +233,8 @@ size_t srcnn_train_workspace_bytes(const srcnn_net* net, uint32_t w, uint32_t h,
   NetDims d;
   if (net_dims(net, w, h, &d) || batch == 0) return 0;
   size_t b = 0;
-  b += 2 * align_up(d.s1 * batch * sizeof(float));  // A1, D1
+  b += align_up(d.s1p * batch * sizeof(float));  // A1
+  b += align_up(d.s1 * batch * sizeof(float));   // D1
   b += 2 * align_up(d.s2 * batch * sizeof(float));  // A2, D2
   b += 2 * align_up(d.s3 * batch * sizeof(float));  // A3, D3
   size_t g = std::max({grad_ws_bytes(1, net->n1, net->f1, d.w1, d.h1, batch),
@@ -266,7 +270,7 @@ int srcnn_train_fwd_bwd(const srcnn_net* net, const float* X, const float* T, ui
   srcnn_net_offsets(net, off);
   char* p = static_cast<char*>(ws);
   float* A1 = reinterpret_cast<float*>(p);
-  p += align_up(d.s1 * batch * sizeof(float));
+  p += align_up(d.s1p * batch * sizeof(float));
   float* D1 = reinterpret_cast<float*>(p);
   p += align_up(d.s1 * batch * sizeof(float));
   float* A2 = reinterpret_cast<float*>(p);

@@ -81,6 +81,12 @@ __device__ unsigned long long g_clk[3][kClockBlocks][2];
 #define SRCNN_L12_PD 4  // L1 X-gather prefetch distance (k-steps); 0 = compiler schedule
 #endif
 constexpr int kL12PD = SRCNN_L12_PD;
+// diagnostics builds only (results invalid): 1 drop the A1 stores, 2 the A2 stores
+#ifdef SRCNN_L12_DIAG
+constexpr int kL12Diag = SRCNN_L12_DIAG;
+#else
+constexpr int kL12Diag = 0;
+#endif
 #ifndef SRCNN_L12_WAVES
 #define SRCNN_L12_WAVES 2  // minimum waves per SIMD (register budget 512 / this)
 #endif
@@ -165,16 +171,20 @@ __global__ __launch_bounds__(256, SRCNN_L12_WAVES) void l12_fwd_kernel(
     f32x16 pa1[NT1], pa2 = zero16();
 #pragma unroll
     for (int t = 0; t < NT1; t++) pa1[t] = zero16();
-    bool pok = false;  // this lane has a pending pixel
+    bool pok = false;    // a chunk is pending (wave-uniform)
+    bool pval = false;   // ... and this lane's pixel is inside the sample (A2)
     float* pa1p = A1;
     float* pa2p = A2;
     auto store_prev = [&](int k) {  // store k of the pending chunk (exec-masked)
       if (pok) {
-        if (k < 4 * NT1) {
+        if (k < 4 * NT1 && !(kL12Diag & 1)) {
+          // blocked A1 (internal to the fused step, read only by d1): block k
+          // of a chunk is 64 lanes x 16 B in lane order, one contiguous 1-KB
+          // store; lanes past the sample store their clamped pixel's copy
           const int t = k / 4, q = k % 4;
-          *reinterpret_cast<float4*>(pa1p + 32 * t + 8 * q) =
+          *reinterpret_cast<float4*>(pa1p + 256 * k) =
               make_float4(pa1[t][4 * q], pa1[t][4 * q + 1], pa1[t][4 * q + 2], pa1[t][4 * q + 3]);
-        } else {
+        } else if (k >= 4 * NT1 && pval && !(kL12Diag & 2)) {
           const int q = k - 4 * NT1;
           *reinterpret_cast<float4*>(pa2p + 8 * q) =
               make_float4(fmaxf(pa2[4 * q], 0.0f), fmaxf(pa2[4 * q + 1], 0.0f),
@@ -236,8 +246,9 @@ __global__ __launch_bounds__(256, SRCNN_L12_WAVES) void l12_fwd_kernel(
 #pragma unroll
       for (int t = 0; t < NT1; t++) pa1[t] = acc1[t];
       pa2 = acc2;
-      pok = pl < npx;
-      pa1p = A1 + ((size_t)sample * npx + pc) * N1 + 4 * h;
+      pok = true;
+      pval = pl < npx;
+      pa1p = A1 + ((size_t)sample * nch + c) * (32 * N1) + 4 * lane;
       pa2p = A2 + ((size_t)sample * npx + pc) * N2 + 4 * h;
     }
 #pragma unroll
@@ -307,12 +318,12 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
   constexpr int KD = N2 / 4;              // delta1 k-steps (over n)
   constexpr int DS = N2 + 4;              // delta2 row in LDS: N2/4 quads + 1 pad quad
   constexpr int WS = N2 + 1;              // padded W2 row in LDS
-  constexpr int A1P = N1 + 4;             // padded A1 row of the LDS image
   constexpr int NW1 = K1 * N1, NW2 = N1 * N2;
   constexpr int P12 = NW1 + N1 + NW2 + N2;  // [gW1 | gB1 | gW2 | gB2]
   static_assert(N2 % 4 == 0 && N1 % 32 == 0 && KR <= 4, "d1 tile shape");
   constexpr int RED1 = MT * NQ * 4 * 64, RED2 = NT1 * NT2 * 16 * 64, REDV = (KR + 1) * NQ * 64;
   constexpr int RED = RED1 + RED2 + REDV;
+  constexpr int A1P = N1 + 4;                  // padded A1 row of the LDS image
   constexpr int A1K = (32 * A1P + 255) / 256;  // 16-byte DMA instructions per A1 chunk
   constexpr int A1S = 256 * A1K;               // per-wave A1 staging
   constexpr int D2S = 32 * DS;                 // per-wave delta2 chunk image [32][DS]
@@ -368,7 +379,8 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
   float* d2me = d2w + wave * D2P;
   float* a1me = a1s + wave * A1S;
   // One LDS-DMA instruction K of a chunk's operands (no registers):
-  //   K < A1K: A1 rows -> this wave's lane-linear [32][A1P] image (16 B / lane;
+  //   K < A1K: A1 block K of the chunk (blocked layout, see l12) -> this
+  //            wave's image, one 1-KB block per instruction (16 B / lane;
   //            the 4-float pad of each row re-reads its first quad)
   //   K >= A1K: delta2 rows -> this wave's padded [32][DS] image (16 B / lane;
   //            the pad quad re-reads quad 0, lanes past the image write into
@@ -386,11 +398,15 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
     const int rmax_ = npx - 1 - (C) * 32;                                         \
     const size_t px0_ = (size_t)(SMP) * npx + (size_t)(C) * 32;                   \
     if ((K) < A1K) {                                                              \
-      const uint32_t f_ = (K) * 256 + 4 * (uint32_t)l_;                           \
-      const uint32_t r_ = f_ / A1P, col_ = f_ - r_ * A1P;                         \
-      const uint32_t off_ = (uint32_t)min((int)r_, rmax_) * N1 + (col_ < N1 ? col_ : 0u); \
+      /* image quad f = row r, quad j of the padded [32][A1P] image (the pad */  \
+      /* re-reads quad 0); in the blocked chunk, quad j of pixel r is lane */    \
+      /* r + 32(j & 1) of block j >> 1: 64-B runs of 4 pixels per half-block */  \
+      const uint32_t f_ = (K) * 64 + (uint32_t)l_;                                \
+      const uint32_t r_ = f_ / (A1P / 4), j0_ = f_ - r_ * (A1P / 4);              \
+      const uint32_t j_ = j0_ < N1 / 4 ? j0_ : 0u;                                \
+      const uint32_t off_ = (j_ >> 1) * 256 + 4 * (min(r_, 31u) + 32 * (j_ & 1u)); \
       __builtin_amdgcn_global_load_lds(                                           \
-          (const void*)(A1 + px0_ * N1 + off_),                                   \
+          (const void*)(A1 + ((size_t)(SMP) * nch + (C)) * (32 * N1) + off_),     \
           (__attribute__((address_space(3))) void*)(a1me + (K) * 256), 16, 0, 0); \
     } else {                                                                      \
       /* delta2 rows, 16 B / lane: slot quad Q of the [32][DS] image is row */   \
@@ -511,6 +527,7 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
 
       // relu' mask of delta1 (after the independent gW2 MFMAs, so the delta1
       // chain has drained without stalling the matrix core)
+
 #pragma unroll
       for (int pm = 0; pm < 2; pm++)
 #pragma unroll
