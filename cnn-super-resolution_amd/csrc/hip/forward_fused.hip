@@ -51,6 +51,13 @@ constexpr int kFwdRW = 32;        // region width (one chunk per region row)
 #define SRCNN_FWD_PD 4  // L1 X-gather prefetch distance (k-steps); 0 = compiler schedule
 #endif
 constexpr int kFwdPD = SRCNN_FWD_PD;
+// diagnostics builds only (results invalid): 1 drop the per-chunk L3 window
+// sums, 2 drop the per-region partial-sum output
+#ifdef SRCNN_FWD_DIAG
+constexpr int kFwdDiag = SRCNN_FWD_DIAG;
+#else
+constexpr int kFwdDiag = 0;
+#endif
 constexpr int kFwdRhMax = SRCNN_FWD_RH;  // region rows (LDS partial-sum accumulator bound)
 constexpr int kFwdXs = (kFwdRhMax + 12) * 40;  // input tile floats staged in LDS (f1 <= 9)
 
@@ -75,13 +82,31 @@ __global__ __launch_bounds__(256, SRCNN_FWD_WAVES) void fwd_l123_kernel(
   constexpr int EHM = kFwdRhMax + F3 - 1;
   static_assert(K3 <= 32 && N2 <= 32 && N2 % 2 == 0 && K1 % 2 == 1, "Q tile shape");
   __shared__ float xs[kFwdXs];
-  __shared__ __attribute__((aligned(16))) float qs[4][32][QS];  // per-wave Q[pixel][tap]
+  // per-wave Q[pixel + F3-1][tap]: F3-1 zero rows either side, so a window
+  // sum reads its F3 taps without bounds tests
+  constexpr int QR = kFwdRW + 2 * (F3 - 1);
+  __shared__ __attribute__((aligned(16))) float qs[4][QR][QS];
   __shared__ float accs[F3][EHM][EW];  // [dy][partial row][partial col]
 
   SRCNN_CLOCK_BEGIN();
   const int lane = mfma::lane_id(), wave = mfma::wave_id();
   const int h = lane >> 5, li = lane & 31;
   const int EH = g.rh + F3 - 1;
+  for (int i = threadIdx.x; i < 4 * 2 * (F3 - 1) * QS; i += 256) {  // the zero rows (never written again)
+    const int w = i / (2 * (F3 - 1) * QS), r = (i / QS) % (2 * (F3 - 1)), col = i % QS;
+    qs[w][r < F3 - 1 ? r : kFwdRW + r][col] = 0.0f;
+  }
+  // L3 window sums: this lane's items k of the F3 x EW (tap row dy, column e)
+  // per chunk, as a base into the wave's Q image (taps dx follow at a stride
+  // of QS + 1 floats) and into the partial-sum accumulator (+ chunk row c * EW)
+  constexpr int kWin = (F3 * EW + 63) / 64;
+  int wrb[kWin], wwb[kWin];
+#pragma unroll
+  for (int k = 0; k < kWin; k++) {
+    const int it = min(lane + 64 * k, F3 * EW - 1), dy = it / EW, e = it - dy * EW;
+    wrb[k] = (wave * QR + e) * QS + dy * F3;
+    wwb[k] = (dy * EHM + F3 - 1 - dy) * EW + e;
+  }
 
   // All three GEMMs run TRANSPOSED (rows = channels / taps, cols = the
   // chunk's 32 pixels), so each layer's accumulator registers are the next
@@ -132,6 +157,7 @@ __global__ __launch_bounds__(256, SRCNN_FWD_WAVES) void fwd_l123_kernel(
     }
   };
   if ((int)blockIdx.x < n_items) xload(blockIdx.x);
+  float diag_sink = 0.0f;  // diagnostics builds: keeps dropped parts' inputs live
   for (int wi = blockIdx.x; wi < n_items; wi += gridDim.x) {
     const int n = wi / per_frame, rr = wi - n * per_frame;
     const int ry = rr / g.nrx;
@@ -196,20 +222,26 @@ __global__ __launch_bounds__(256, SRCNN_FWD_WAVES) void fwd_l123_kernel(
       // Q[pixel li][taps crow(r, h)]: 4 runs of 4 consecutive taps per lane
 #pragma unroll
       for (int q = 0; q < 4; q++)
-        *reinterpret_cast<float4*>(&qs[wave][li][8 * q + 4 * h]) =
+        *reinterpret_cast<float4*>(&qs[wave][li + F3 - 1][8 * q + 4 * h]) =
             make_float4(accq[4 * q], accq[4 * q + 1], accq[4 * q + 2], accq[4 * q + 3]);
       __builtin_amdgcn_wave_barrier();
       // tap row dy of this chunk feeds partial row c + F3 - 1 - dy:
       //   accs[dy][c + F3-1 - dy][e] = sum_dx Q[e - (F3-1) + dx][dy*F3 + dx]
-      for (int i = lane; i < F3 * EW; i += 64) {
-        const int dy = i / EW, e = i - dy * EW;
-        float v = 0.0f;
+      if (kFwdDiag & 1) {  // keep Q alive without its window sums
 #pragma unroll
-        for (int dx = 0; dx < F3; dx++) {
-          const int px = e - (F3 - 1) + dx;
-          if (px >= 0 && px < kFwdRW) v += qs[wave][px][dy * F3 + dx];
+        for (int r = 0; r < 16; r++) diag_sink += accq[r];
+      }
+      //   (Q row e + dx of the padded image is pixel e - (F3-1) + dx)
+#pragma unroll
+      for (int k = 0; k < kWin; k++) {
+        if (kFwdDiag & 1) break;
+        if (k < kWin - 1 || lane + 64 * k < F3 * EW) {
+          const float* qr = &qs[0][0][0] + wrb[k];
+          float v = 0.0f;
+#pragma unroll
+          for (int dx = 0; dx < F3; dx++) v += qr[dx * (QS + 1)];
+          (&accs[0][0][0])[wwb[k] + c * EW] = v;
         }
-        accs[dy][c + F3 - 1 - dy][e] = v;
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_wave_barrier();
@@ -225,9 +257,11 @@ __global__ __launch_bounds__(256, SRCNN_FWD_WAVES) void fwd_l123_kernel(
         const int c = pr - (F3 - 1) + dy;
         if (c >= 0 && c < crh) v += accs[dy][pr][e];
       }
-      dst[i] = v;
+      if (!(kFwdDiag & 2)) dst[i] = v;
+      else diag_sink += v;
     }
   }
+  if (kFwdDiag && diag_sink == 1234.5f) part[threadIdx.x] = diag_sink;
   SRCNN_CLOCK_END(g_clk_fwd, 0);
 }
 
