@@ -69,11 +69,13 @@ def split_ws(ws, w, h, batch):
     w1, h1 = w - f1 + 1, h - f1 + 1
     w2, h2 = w1 - f2 + 1, h1 - f2 + 1
     s1, s2 = w1 * h1 * n1 * batch, w2 * h2 * n2 * batch
+    # the A1 region holds whole 32-pixel chunks per sample (abi.cpp NetDims::s1p)
+    s1p = (w1 * h1 + 31) // 32 * 32 * n1 * batch
     o = 0
     out = {}
-    for name, n in (("A1", s1), ("D1", s1), ("A2", s2), ("D2", s2)):
+    for name, n, room in (("A1", s1, s1p), ("D1", s1, s1), ("A2", s2, s2), ("D2", s2, s2)):
         out[name] = ws[o // 4:o // 4 + n]
-        o += align(4 * n)
+        o += align(4 * room)
     return out
 
 
