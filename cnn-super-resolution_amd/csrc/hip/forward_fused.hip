@@ -51,8 +51,10 @@ constexpr int kFwdRW = 32;        // region width (one chunk per region row)
 #define SRCNN_FWD_PD 4  // L1 X-gather prefetch distance (k-steps); 0 = compiler schedule
 #endif
 constexpr int kFwdPD = SRCNN_FWD_PD;
+
 // diagnostics builds only (results invalid): 1 drop the per-chunk L3 window
-// sums, 2 drop the per-region partial-sum output
+// sums, 2 drop the per-region partial-sum output, 4 drop the ReLUs, 8 drop the
+// next region's register-staged input loads
 #ifdef SRCNN_FWD_DIAG
 constexpr int kFwdDiag = SRCNN_FWD_DIAG;
 #else
@@ -171,7 +173,7 @@ __global__ __launch_bounds__(256, SRCNN_FWD_WAVES) void fwd_l123_kernel(
       if (i < kFwdXs) xs[i] = xr[k];
     }
     __syncthreads();
-    if (wi + (int)gridDim.x < n_items) xload(wi + gridDim.x);
+    if (wi + (int)gridDim.x < n_items && !(kFwdDiag & 8)) xload(wi + gridDim.x);
 
     for (int c = wave; c < crh; c += 4) {  // chunk = region row c, pixel li
       // tap 2s+1 sits 1 or TW - F1 + 1 floats past tap 2s: two per-half bases,
@@ -205,7 +207,8 @@ __global__ __launch_bounds__(256, SRCNN_FWD_WAVES) void fwd_l123_kernel(
 #pragma unroll
       for (int t = 0; t < NT1; t++)
 #pragma unroll
-        for (int r = 0; r < 16; r++) acc1[t][r] = fmaxf(acc1[t][r], 0.0f);
+        for (int r = 0; r < 16; r++)
+          if (!(kFwdDiag & 4)) acc1[t][r] = fmaxf(acc1[t][r], 0.0f);
       // L2^T: A2^T[n][p] = B2[n] + sum_c W2[c][n] A1^T[c][p], then ReLU
       f32x16 acc2 = zero16();
       acc2 = mma(b2a, 1.0f, acc2);
@@ -214,7 +217,8 @@ __global__ __launch_bounds__(256, SRCNN_FWD_WAVES) void fwd_l123_kernel(
 #pragma unroll
         for (int s = 0; s < 16; s++) acc2 = mma(w2f[t][s], acc1[t][s], acc2);
 #pragma unroll
-      for (int r = 0; r < 16; r++) acc2[r] = fmaxf(acc2[r], 0.0f);
+      for (int r = 0; r < 16; r++)
+        if (!(kFwdDiag & 4)) acc2[r] = fmaxf(acc2[r], 0.0f);
       // Q^T[tap][p] = sum_c W3[tap][c] A2^T[c][p]
       f32x16 accq = zero16();
 #pragma unroll
