@@ -489,6 +489,9 @@ __global__ __launch_bounds__(256) void wl3_kernel(const float* __restrict__ A2,
   extern __shared__ float smem[];
   float* Qs = smem;             // [npx2][FF], later the cross-wave reduction
   float* Gd = smem + qfloats;   // [(h3 + 2(F3-1))][(w3 + 2(F3-1))]
+  // relu' mask of A2 as bits, built from the step-1 operand registers so step
+  // 3 does not re-read A2 from HBM: word [p][h] bit 4kk + jj <-> channel 8kk + 4h + jj
+  unsigned* mbits = reinterpret_cast<unsigned*>(Gd + (g.w3 + 2 * (F3 - 1)) * (g.h3 + 2 * (F3 - 1)));
   __shared__ float red_s[2][4];
   const int lane = lane_id(), wave = wave_id(), j = lane & 31, h = lane >> 5;
   const int npx2 = g.w2 * g.h2, mt2 = (npx2 + 31) / 32, npx3 = g.w3 * g.h3;
@@ -533,6 +536,14 @@ __global__ __launch_bounds__(256) void wl3_kernel(const float* __restrict__ A2,
       for (int kk = 0; kk < 8; kk++)
 #pragma unroll
         for (int jj = 0; jj < 4; jj++) acc = mma(v[kk][jj], wq[kk][jj], acc);
+      {
+        unsigned m = 0;
+#pragma unroll
+        for (int kk = 0; kk < 8; kk++)
+#pragma unroll
+          for (int jj = 0; jj < 4; jj++) m |= (v[kk][jj] > 0.0f ? 1u : 0u) << (4 * kk + jj);
+        if (32 * mt + j < npx2) mbits[2 * (32 * mt + j) + h] = m;
+      }
 #pragma unroll
       for (int r = 0; r < 16; r++) {
         const int pix = 32 * mt + crow(r, h);
@@ -556,7 +567,8 @@ __global__ __launch_bounds__(256) void wl3_kernel(const float* __restrict__ A2,
       Gd[(oy + F3 - 1) * GW + ox + F3 - 1] = d;
     }
     __syncthreads();
-    // 3. delta2
+    // 3. delta2 (channel 32nt + j: mask word half mh, bit mbit)
+    const int mc = 32 * nt + j, mh = (mc >> 2) & 1, mbit = 4 * (mc >> 3) + (mc & 3);
     for (int mt = mg; mt < mt2; mt += 2) {
       const int p = min(32 * mt + j, npx2 - 1), py = p / g.w2, px = p - py * g.w2;
       const int gb = (py + F3 - 1) * GW + px + F3 - 1;
@@ -568,7 +580,7 @@ __global__ __launch_bounds__(256) void wl3_kernel(const float* __restrict__ A2,
         const int pix = 32 * mt + crow(r, h);
         if (pix < npx2) {
           const size_t idx = ((size_t)s * npx2 + pix) * N2 + 32 * nt + j;
-          D2[idx] = A2[idx] > 0.0f ? acc[r] : 0.0f;
+          D2[idx] = (mbits[2 * pix + mh] >> mbit) & 1u ? acc[r] : 0.0f;
         }
       }
     }
@@ -782,7 +794,7 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   g2.groups = (int)std::min<uint32_t>(batch, 64);
   // wl3 LDS
   const int qfloats = std::max(npx2 * F3 * F3, 2 * 16 * 64 * 4);
-  const size_t lds3 = (size_t)(qfloats + (g.w3 + 2 * (F3 - 1)) * (g.h3 + 2 * (F3 - 1))) * 4;
+  const size_t lds3 = (size_t)(qfloats + (g.w3 + 2 * (F3 - 1)) * (g.h3 + 2 * (F3 - 1)) + 2 * npx2) * 4;
   if (lds3 > 64 * 1024) return 0;
   constexpr int NPD = N1 / 64;  // delta1 items per sample (64-channel parts)
   const int GD = std::min(g.batch * NPD, 256);  // a multiple of NPD: block parity = part
