@@ -219,6 +219,13 @@ constexpr int kXBuf = kXTile + 64;  // X tile buffer of the fused gW1 epilogue
 // leaves the CU; A = X windows (81 taps + a ones row for gB1, 3 x 32 rows)
 // from a per-item X tile DMA'd into LDS.  One gW1 slab per pair of blocks
 // (block parity = the 64-channel part, fixed because the grid is even).
+// diagnostics builds only (results invalid), delta1 + gW1 variant: 1 drop the
+// gW1 MFMAs, 2 drop the relu' mask loads, 4 drop the next-chunk LDS-DMA
+#ifdef SRCNN_WIDE_DIAG
+constexpr int kWDiag = SRCNN_WIDE_DIAG;
+#else
+constexpr int kWDiag = 0;
+#endif
 template <int CIN, int COUT, int F, int MT, bool DELTA, int F1>
 __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restrict__ in,
                                                           const float* __restrict__ Wimg,
@@ -338,7 +345,7 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restri
 #pragma unroll
           for (int q = 0; q < 2; q++) {
             const int k = wave + 4 * (2 * t + q);
-            if (stage && k < kdma) dma(nit, nc, nxt, k);
+            if (stage && k < kdma && !(kWDiag & 4)) dma(nit, nc, nxt, k);
           }
           // k-step (t, 0) while (t, 1) loads; k-step (t, 1) while (t + 1, 0)
           // loads.  sched_barriers pin the order: left alone, the scheduler
@@ -381,7 +388,7 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restri
 #pragma unroll
       for (int r = 0; r < 16; r++) {
         const int pix = min(32 * mg + crow(r, h), g.npx - 1);
-        mk[r] = ycur[obase + (size_t)pix * COUT];
+        mk[r] = (kWDiag & 2) ? 1.0f : ycur[obase + (size_t)pix * COUT];
       }
 #pragma unroll
       for (int m = 0; m < MT; m++) {
@@ -392,7 +399,7 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restri
 #pragma unroll
           for (int r = 0; r < 16; r++) {
             const int pix = min(p0 + 64 + crow(r, 0), g.npx - 1);
-            mkn[r] = ycur[obase + (size_t)pix * COUT];
+            mkn[r] = (kWDiag & 2) ? 1.0f : ycur[obase + (size_t)pix * COUT];
           }
         }
 #pragma unroll
@@ -407,7 +414,8 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restri
 #pragma unroll
           for (int tt = 0; tt < TT; tt++) {
             const float av = xs[xb + toffx[tt]];
-            gacc[tt] = mma(valid[tt] ? av : fill[tt], acc[m][r], gacc[tt]);
+            if (!(kWDiag & 1)) gacc[tt] = mma(valid[tt] ? av : fill[tt], acc[m][r], gacc[tt]);
+            else gacc[tt][0] += acc[m][r] + av;
           }
         }
         if (m + 1 < MT) {
