@@ -16,9 +16,9 @@ ok $rc || exit $rc
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
 rc=$?; echo "smoke rc=$rc"; tail -3 "$OUT/smoke.log"
 [ $rc -eq 0 ] || exit $rc
-timeout -k 10 600 python bench.py --steps ${BENCH_STEPS:-20} --warmup 3 > "$OUT/bench.json" 2> "$OUT/bench.err"
+timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > "$OUT/bench.json" 2> "$OUT/bench.err"
 rc=$?; echo "bench rc=$rc"; cat "$OUT/bench.json"; tail -3 "$OUT/bench.err"
 [ $rc -eq 0 ] || exit $rc
-cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$OUT/rocprof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps ${BENCH_STEPS:-20} --warmup 3 --no-cpu-baseline > "$GRAFT_REPO_ROOT/$OUT/rocprof_bench.log" 2>&1
+cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$OUT/rocprof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" ${BENCH_ARGS:-} --no-cpu-baseline > "$GRAFT_REPO_ROOT/$OUT/rocprof_bench.log" 2>&1
 rc=$?; echo "rocprof rc=$rc"
 exit $rc
