@@ -210,7 +210,8 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
         const int q_ = j_ ^ ((p_ >> 1) & (NQ - 1));                                      \
         __builtin_amdgcn_global_load_lds(                                                \
             (const void*)(src_ + p_ * N2 + 4 * q_),                                      \
-            (__attribute__((address_space(3))) void*)((DST) + 256 * k_), 16, 0, 0);      \
+            (__attribute__((address_space(3))) void*)((DST) + 256 * k_), 16, 0,          \
+            (kNtMask & 1) ? 2 : 0);                                                      \
       }                                                                                  \
     }                                                                                    \
   } while (0)
@@ -238,7 +239,10 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
     if (d2pend && q_ < npx2 && !kL3DiagNoStore) {                                      \
       float* dst_ = d2dst + (size_t)q_ * N2 + 4 * lg;                                  \
       _Pragma("unroll") for (int t = 0; t < NT; t++)                                   \
-        *reinterpret_cast<f32x4*>(dst_ + 16 * t) = d2k[J][t];                          \
+        if (kNtMask & 2)                                                               \
+          __builtin_nontemporal_store(d2k[J][t], reinterpret_cast<f32x4*>(dst_ + 16 * t)); \
+        else                                                                           \
+          *reinterpret_cast<f32x4*>(dst_ + 16 * t) = d2k[J][t];                        \
     }                                                                                  \
   } while (0)
 

@@ -77,6 +77,16 @@ __device__ unsigned long long g_clk[3][kClockBlocks][2];
 #ifndef SRCNN_L12_GRID
 #define SRCNN_L12_GRID 1024  // grid cap (blocks), a multiple of 256 CUs x blocks per CU
 #endif
+// streaming-cache hints (bits): 1 l3 A2 DMA nt, 2 l3 D2 stores nt, 4 d1
+// operand DMA nt, 8 l12 A1 stores nt.  Default 1 | 8 (same-box A/B, steady
+// state, 2 reps: step 0.938 -> 0.931 ms): A1 (655 MB per step, read back only
+// by d1) streams past the caches, so more of the A2 that l12 writes just
+// before l3 reads it stays in the 256 MB MALL (l3 -4.5%); nt on the D2
+// stores or the d1 DMA was slower.
+#ifndef SRCNN_NT
+#define SRCNN_NT 9
+#endif
+constexpr int kNtMask = SRCNN_NT;
 #ifndef SRCNN_L12_PD
 #define SRCNN_L12_PD 4  // L1 X-gather prefetch distance (k-steps); 0 = compiler schedule
 #endif
@@ -182,8 +192,15 @@ __global__ __launch_bounds__(256, SRCNN_L12_WAVES) void l12_fwd_kernel(
           // of a chunk is 64 lanes x 16 B in lane order, one contiguous 1-KB
           // store; lanes past the sample store their clamped pixel's copy
           const int t = k / 4, q = k % 4;
-          *reinterpret_cast<float4*>(pa1p + 256 * k) =
-              make_float4(pa1[t][4 * q], pa1[t][4 * q + 1], pa1[t][4 * q + 2], pa1[t][4 * q + 3]);
+          if (kNtMask & 8) {
+            f32x4 v_;
+#pragma unroll
+            for (int e = 0; e < 4; e++) v_[e] = pa1[t][4 * q + e];
+            __builtin_nontemporal_store(v_, reinterpret_cast<f32x4*>(pa1p + 256 * k));
+          } else {
+            *reinterpret_cast<float4*>(pa1p + 256 * k) =
+                make_float4(pa1[t][4 * q], pa1[t][4 * q + 1], pa1[t][4 * q + 2], pa1[t][4 * q + 3]);
+          }
         } else if (k >= 4 * NT1 && pval && !(kL12Diag & 2)) {
           const int q = k - 4 * NT1;
           *reinterpret_cast<float4*>(pa2p + 8 * q) =
@@ -407,7 +424,8 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
       const uint32_t off_ = (j_ >> 1) * 256 + 4 * (min(r_, 31u) + 32 * (j_ & 1u)); \
       __builtin_amdgcn_global_load_lds(                                           \
           (const void*)(A1 + ((size_t)(SMP) * nch + (C)) * (32 * N1) + off_),     \
-          (__attribute__((address_space(3))) void*)(a1me + (K) * 256), 16, 0, 0); \
+          (__attribute__((address_space(3))) void*)(a1me + (K) * 256), 16, 0,      \
+          (kNtMask & 4) ? 2 : 0);                                                 \
     } else {                                                                      \
       /* delta2 rows, 16 B / lane: slot quad Q of the [32][DS] image is row */   \
       /* Q / (DS/4), quad Q % (DS/4); the pad quad re-reads quad 0 */            \
@@ -416,7 +434,8 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
       const uint32_t off_ = (uint32_t)min((int)r_, rmax_) * N2 + (j_ < N2 / 4 ? 4 * j_ : 0u); \
       __builtin_amdgcn_global_load_lds(                                           \
           (const void*)(D2 + px0_ * N2 + off_),                                   \
-          (__attribute__((address_space(3))) void*)(d2me + 256 * ((K) - A1K)), 16, 0, 0); \
+          (__attribute__((address_space(3))) void*)(d2me + 256 * ((K) - A1K)), 16, 0, \
+          (kNtMask & 4) ? 2 : 0);                                                 \
     }                                                                             \
   } while (0)
 #define SRCNN_D1_DMA_ALL(SMP, C)                                                  \

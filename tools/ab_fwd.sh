@@ -19,7 +19,7 @@ for rep in 1 2; do
   i=0
   for lib in "$@"; do
     i=$((i+1))
-    SRCNN_HIP_LIB=$PWD/$lib timeout -k 10 180 python bench.py --steps 30 --warmup 5 --no-cpu-baseline ${AB_ARGS:---no-wide} > "$OUT/bench_${i}_$rep.json" 2>"$OUT/bench_${i}_$rep.err" || exit $?
+    SRCNN_HIP_LIB=$PWD/$lib timeout -k 10 180 python bench.py --no-cpu-baseline ${AB_ARGS:---no-wide} > "$OUT/bench_${i}_$rep.json" 2>"$OUT/bench_${i}_$rep.err" || exit $?
     python3 -c "import json; d=json.load(open('$OUT/bench_${i}_$rep.json')); print('variant $i rep $rep', round(d['value']), d['ms_per_step'], {k:round(v['ms_per_step'],4) for k,v in d['kernels'].items()}, 'fwd', d.get('forward',{}).get('ms_per_frame'), d.get('forward',{}).get('kernels'))"
   done
 done
