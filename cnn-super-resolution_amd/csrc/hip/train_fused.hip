@@ -320,6 +320,10 @@ constexpr int kD1Diag = 0;
 #endif
 constexpr bool kD1DiagNoD1 = kD1Diag & 1, kD1DiagNoGW2 = kD1Diag & 2, kD1DiagNoMask = kD1Diag & 4,
                kD1DiagNoGW1 = kD1Diag & 8, kD1DiagNoDma = kD1Diag & 16;
+#ifndef SRCNN_D1_A1SW
+#define SRCNN_D1_A1SW 1
+#endif
+constexpr bool kD1A1Sw = SRCNN_D1_A1SW;
 #ifndef SRCNN_D1_TOPWAIT
 #define SRCNN_D1_TOPWAIT 1  // sample top waits for the X tile only, not the next chunk's operands
 #endif
@@ -329,6 +333,8 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
     const float* __restrict__ X, const float* __restrict__ A1, const float* __restrict__ D2,
     const float* __restrict__ W2, float* __restrict__ slab, Geom g) {
   constexpr int K1 = F1 * F1, NT1 = N1 / 32, NT2 = (N2 + 31) / 32;
+  // quad swizzle of A1 image row r (bits 2 and 3 of r -> quad bits 3 and 2)
+  auto a1sw = [](int r) { return ((((r >> 2) & 1) << 3) | (((r >> 3) & 1) << 2)) & (N1 / 4 - 1); };
   constexpr int NQ = N1 / 16;             // 16-wide channel tiles
   constexpr int MT = K1 / 16;             // 16-tap MFMA tiles
   constexpr int KR = K1 - 16 * MT;        // taps left to the VALU
@@ -340,7 +346,11 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
   static_assert(N2 % 4 == 0 && N1 % 32 == 0 && KR <= 4, "d1 tile shape");
   constexpr int RED1 = MT * NQ * 4 * 64, RED2 = NT1 * NT2 * 16 * 64, REDV = (KR + 1) * NQ * 64;
   constexpr int RED = RED1 + RED2 + REDV;
-  constexpr int A1P = N1 + 4;                  // padded A1 row of the LDS image
+  // A1 LDS image rows: SRCNN_D1_A1SW = 1: N1 floats with the 16-B quads of
+  // row r XOR-swizzled by a1sw(r) (8 * bit 2 + 4 * bit 3 of r); 0: rows
+  // padded by one quad.  Both make the gW2 and mask reads conflict-free;
+  // the swizzle saves one DMA instruction per chunk.
+  constexpr int A1P = kD1A1Sw ? N1 : N1 + 4;
   constexpr int A1K = (32 * A1P + 255) / 256;  // 16-byte DMA instructions per A1 chunk
   constexpr int A1S = 256 * A1K;               // per-wave A1 staging
   constexpr int D2S = 32 * DS;                 // per-wave delta2 chunk image [32][DS]
@@ -415,12 +425,13 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
     const int rmax_ = npx - 1 - (C) * 32;                                         \
     const size_t px0_ = (size_t)(SMP) * npx + (size_t)(C) * 32;                   \
     if ((K) < A1K) {                                                              \
-      /* image quad f = row r, quad j of the padded [32][A1P] image (the pad */  \
-      /* re-reads quad 0); in the blocked chunk, quad j of pixel r is lane */    \
-      /* r + 32(j & 1) of block j >> 1: 64-B runs of 4 pixels per half-block */  \
+      /* image quad f = row r, slot q of the [32][A1P] image (padded: the pad */ \
+      /* re-reads quad 0; swizzled: slot q holds quad q ^ a1sw(r)); in the */    \
+      /* blocked chunk, quad j of pixel r is lane r + 32(j & 1) of block */      \
+      /* j >> 1: 64-B runs of 4 pixels per half-block */                         \
       const uint32_t f_ = (K) * 64 + (uint32_t)l_;                                \
       const uint32_t r_ = f_ / (A1P / 4), j0_ = f_ - r_ * (A1P / 4);              \
-      const uint32_t j_ = j0_ < N1 / 4 ? j0_ : 0u;                                \
+      const uint32_t j_ = kD1A1Sw ? (j0_ ^ (uint32_t)a1sw(r_)) : (j0_ < N1 / 4 ? j0_ : 0u); \
       const uint32_t off_ = (j_ >> 1) * 256 + 4 * (min(r_, 31u) + 32 * (j_ & 1u)); \
       __builtin_amdgcn_global_load_lds(                                           \
           (const void*)(A1 + ((size_t)(SMP) * nch + (C)) * (32 * N1) + off_),     \
@@ -530,6 +541,18 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
       }
       SRCNN_D1_TICK(2);
       // gW2[c][n] += sum_p A1[p][c] delta2[p][n]; gB2[n] += sum_p delta2[p][n]
+      // swizzled image: pixel crow(s, h), channel 32t + li sits at
+      // gw2b[t][bit 2 of s] + ((s & 3) + 8 (s >> 2)) A1P (crow's bit 2 is h)
+      int gw2b[NT1][2];
+      {
+        int li_ = li;
+        asm volatile("" : "+v"(li_));
+#pragma unroll
+        for (int t = 0; t < NT1; t++)
+#pragma unroll
+          for (int sb = 0; sb < 2; sb++)
+            gw2b[t][sb] = 4 * h * A1P + 4 * ((8 * t + (li_ >> 2)) ^ a1sw(4 * h + 8 * sb)) + (li_ & 3);
+      }
 #pragma unroll
       for (int s = 0; s < 16; s++) {
         const int pr = crow(s, h);
@@ -540,12 +563,18 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
           gb2[u] += b;
 #pragma unroll
           for (int t = 0; t < NT1; t++)
-            if (!kD1DiagNoGW2) g2[t][u] = mma(a1me[pr * A1P + 32 * t + li], b, g2[t][u]);
+            if (!kD1DiagNoGW2)
+              g2[t][u] = mma(a1me[kD1A1Sw ? gw2b[t][(s >> 2) & 1] + ((s & 3) + 8 * (s >> 2)) * A1P
+                                          : pr * A1P + 32 * t + li],
+                             b, g2[t][u]);
         }
       }
 
       // relu' mask of delta1 (after the independent gW2 MFMAs, so the delta1
-      // chain has drained without stalling the matrix core)
+      // chain has drained without stalling the matrix core); swizzled image:
+      // row 16pm + 4lg + i, channel 16t + lq sits at mskb ^ 16t + (16pm + i) A1P
+      int mskb = 4 * lg * A1P + 16 * (a1sw(4 * lg) >> 2) + 4 * (lq >> 2) + (lq & 3);
+      asm volatile("" : "+v"(mskb));
 
 #pragma unroll
       for (int pm = 0; pm < 2; pm++)
@@ -554,7 +583,10 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
 #pragma unroll
           for (int i = 0; i < 4; i++)
             if (!kD1DiagNoMask)
-              d1[pm][t][i] = a1me[(16 * pm + 4 * lg + i) * A1P + 16 * t + lq] > 0.0f ? d1[pm][t][i] : 0.0f;
+              d1[pm][t][i] = a1me[kD1A1Sw ? (mskb ^ (16 * t)) + (16 * pm + i) * A1P
+                                          : (16 * pm + 4 * lg + i) * A1P + 16 * t + lq] > 0.0f
+                                 ? d1[pm][t][i]
+                                 : 0.0f;
 
       SRCNN_D1_TICK(3);
       // next chunk's operand DMA overlaps the gW1 MFMAs (the images' reads retired)
