@@ -320,6 +320,10 @@ constexpr int kD1Diag = 0;
 #endif
 constexpr bool kD1DiagNoD1 = kD1Diag & 1, kD1DiagNoGW2 = kD1Diag & 2, kD1DiagNoMask = kD1Diag & 4,
                kD1DiagNoGW1 = kD1Diag & 8, kD1DiagNoDma = kD1Diag & 16;
+#ifndef SRCNN_D1_D2SW
+#define SRCNN_D1_D2SW 1
+#endif
+constexpr bool kD1D2Sw = SRCNN_D1_D2SW;
 #ifndef SRCNN_D1_A1SW
 #define SRCNN_D1_A1SW 1
 #endif
@@ -335,11 +339,15 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
   constexpr int K1 = F1 * F1, NT1 = N1 / 32, NT2 = (N2 + 31) / 32;
   // quad swizzle of A1 image row r (bits 2 and 3 of r -> quad bits 3 and 2)
   auto a1sw = [](int r) { return ((((r >> 2) & 1) << 3) | (((r >> 3) & 1) << 2)) & (N1 / 4 - 1); };
+  // quad swizzle of delta2 image row r
+  auto d2sw = [](int r) { return (r >> 1) & (N2 / 4 - 1); };
   constexpr int NQ = N1 / 16;             // 16-wide channel tiles
   constexpr int MT = K1 / 16;             // 16-tap MFMA tiles
   constexpr int KR = K1 - 16 * MT;        // taps left to the VALU
   constexpr int KD = N2 / 4;              // delta1 k-steps (over n)
-  constexpr int DS = N2 + 4;              // delta2 row in LDS: N2/4 quads + 1 pad quad
+  // delta2 LDS image rows: SRCNN_D1_D2SW = 1: N2 floats, quads of row r
+  // XOR-swizzled by d2sw(r) = (r >> 1) mod N2/4; 0: one pad quad per row
+  constexpr int DS = kD1D2Sw ? N2 : N2 + 4;
   constexpr int WS = N2 + 1;              // padded W2 row in LDS
   constexpr int NW1 = K1 * N1, NW2 = N1 * N2;
   constexpr int P12 = NW1 + N1 + NW2 + N2;  // [gW1 | gB1 | gW2 | gB2]
@@ -439,9 +447,11 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
           (kNtMask & 4) ? 2 : 0);                                                 \
     } else {                                                                      \
       /* delta2 rows, 16 B / lane: slot quad Q of the [32][DS] image is row */   \
-      /* Q / (DS/4), quad Q % (DS/4); the pad quad re-reads quad 0 */            \
+      /* Q / (DS/4), slot Q % (DS/4) (swizzled: quad slot ^ d2sw(row); */        \
+      /* padded: the pad quad re-reads quad 0) */                                \
       const uint32_t q_ = 64 * ((K) - A1K) + (uint32_t)l_;                        \
-      const uint32_t r_ = q_ / (DS / 4), j_ = q_ - r_ * (DS / 4);                 \
+      const uint32_t r_ = q_ / (DS / 4), j0_ = q_ - r_ * (DS / 4);                \
+      const uint32_t j_ = kD1D2Sw ? (j0_ ^ (uint32_t)d2sw(r_)) : j0_;             \
       const uint32_t off_ = (uint32_t)min((int)r_, rmax_) * N2 + (j_ < N2 / 4 ? 4 * j_ : 0u); \
       __builtin_amdgcn_global_load_lds(                                           \
           (const void*)(D2 + px0_ * N2 + off_),                                   \
@@ -525,12 +535,16 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
         for (int t = 0; t < NQ; t++) d1[pm][t] = mfma::zero4();
       // (Measured slower: these operands read one delta1/gW2 super-step ahead
       // into two register sets pinned by sched barriers -- 3 VGPR spills.)
+      // swizzled delta2 image: row 16pm + lq, channel 4s + lg at dab ^ 4s + 16pm DS
+      int dab = lq * DS + 4 * d2sw(lq) + lg;
+      asm volatile("" : "+v"(dab));
 #pragma unroll
       for (int s = 0; s < KD; s++) {
         const int n = 4 * s + lg;
         float a[2], b[NQ];
 #pragma unroll
-        for (int pm = 0; pm < 2; pm++) a[pm] = d2me[(16 * pm + lq) * DS + n];
+        for (int pm = 0; pm < 2; pm++)
+          a[pm] = d2me[kD1D2Sw ? (dab ^ (4 * s)) + 16 * pm * DS : (16 * pm + lq) * DS + n];
 #pragma unroll
         for (int t = 0; t < NQ; t++) b[t] = w2s[(16 * t + lq) * WS + n];
 #pragma unroll
@@ -543,6 +557,9 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
       // gW2[c][n] += sum_p A1[p][c] delta2[p][n]; gB2[n] += sum_p delta2[p][n]
       // swizzled image: pixel crow(s, h), channel 32t + li sits at
       // gw2b[t][bit 2 of s] + ((s & 3) + 8 (s >> 2)) A1P (crow's bit 2 is h)
+      // swizzled delta2 image: pixel pr0 + 4h, channel li at gdb ^ 4 d2sw(pr0) + pr0 DS
+      int gdb = 4 * h * DS + 4 * ((li >> 2) ^ ((2 * h) & (N2 / 4 - 1))) + (li & 3);
+      asm volatile("" : "+v"(gdb));
       int gw2b[NT1][2];
       {
         int li_ = li;
@@ -559,7 +576,8 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
 #pragma unroll
         for (int u = 0; u < NT2; u++) {
           const int n = 32 * u + li;
-          const float b = n < N2 ? d2me[pr * DS + n] : 0.0f;
+          const int pr0 = (s & 3) + 8 * (s >> 2);  // crow(s, 0); pr = pr0 + 4h
+          const float b = n < N2 ? d2me[kD1D2Sw ? (gdb ^ (4 * d2sw(pr0))) + pr0 * DS : pr * DS + n] : 0.0f;
           gb2[u] += b;
 #pragma unroll
           for (int t = 0; t < NT1; t++)
