@@ -26,8 +26,8 @@ PASSES=${PMC_PASSES:-fetch write sq1 sq2 sq3 tcc}
 want() { case " $PASSES " in *" $1 "*) return 0;; esac; return 1; }
 want fetch && { run_pass fetch FETCH_SIZE || exit $?; }
 want write && { run_pass write WRITE_SIZE || exit $?; }
-want sq1 && run_pass sq1 SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT || exit $?
-want sq2 && run_pass sq2 SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR || exit $?
-want sq3 && run_pass sq3 SQ_INSTS_VALU_MFMA_F32 SQ_INSTS_MFMA SQ_LDS_UNALIGNED_STALL SQ_INSTS_SMEM SQ_WAVES SQ_INSTS_VALU_FMA_F32 || exit $?
-want tcc && run_pass tcc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum || exit $?
+want sq1 && { run_pass sq1 SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT || exit $?; }
+want sq2 && { run_pass sq2 SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR || exit $?; }
+want sq3 && { run_pass sq3 SQ_INSTS_VALU_MFMA_F32 SQ_INSTS_MFMA SQ_LDS_UNALIGNED_STALL SQ_INSTS_SMEM SQ_WAVES SQ_INSTS_VALU_FMA_F32 || exit $?; }
+want tcc && { run_pass tcc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum || exit $?; }
 echo done
