@@ -57,6 +57,15 @@ constexpr bool kL3DiagNoGW3 = true;
 constexpr bool kL3DiagNoGW3 = false;
 #endif
 
+// Sample order: l3 walks the batch from the end.  l12 wrote the last
+// samples' A2 last, so they are the ones still in the MALL; and l3's own last
+// D2 rows are then the batch head, which d1 (grid-strided from the start)
+// reads first.
+#ifndef SRCNN_L3_REVERSE
+#define SRCNN_L3_REVERSE 1
+#endif
+__device__ __forceinline__ int l3_order(int s, int batch) { return SRCNN_L3_REVERSE ? batch - 1 - s : s; }
+
 struct L3Geom {
   int W, H;     // ground-truth sample (= network input size)
   int w2, h2;   // A2
@@ -248,8 +257,8 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
 
   int cur = 0;
   if ((int)blockIdx.x < g.batch) {
-    SRCNN_L3_A2_DMA(blockIdx.x, smem);
-    SRCNN_L3_T_PREFETCH(blockIdx.x);
+    SRCNN_L3_A2_DMA(l3_order(blockIdx.x, g.batch), smem);
+    SRCNN_L3_T_PREFETCH(l3_order(blockIdx.x, g.batch));
   }
 #ifdef SRCNN_L3_TIMING
   unsigned long long tacc[4] = {0, 0, 0, 0}, tlast = clock64();
@@ -268,7 +277,7 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
 #pragma unroll
     for (int k = 0; k < kL3TPF; k++) tcur[k] = tpf[k];
     const bool has_next = sample + (int)gridDim.x < g.batch;
-    if (has_next) SRCNN_L3_T_PREFETCH(sample + gridDim.x);
+    if (has_next) SRCNN_L3_T_PREFETCH(l3_order(sample + gridDim.x, g.batch));
 
     // ---- Q = A2 . W3^T per 16-pixel unit (rows past npx2 are discarded);
     // the PREVIOUS sample's masked delta2 leaves to HBM under these MFMAs ----
@@ -334,7 +343,7 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
     // (Measured slower: loading the next A2 into registers under the Q MFMAs
     // and writing it here, so its HBM reads leave the delta2 phase.)
 #ifndef SRCNN_L3_DIAG_NODMA
-    if (has_next) SRCNN_L3_A2_DMA(sample + gridDim.x, other);
+    if (has_next) SRCNN_L3_A2_DMA(l3_order(sample + gridDim.x, g.batch), other);
 #endif
 
     // ---- per 16-pixel unit: delta2 and gW3 MFMAs ----
@@ -392,7 +401,7 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
           for (int i = 0; i < 4; i++) d2k[j][t][i] = mk[t][i] > 0.0f ? acc[t][i] : 0.0f;
       }
     }
-    d2dst = D2 + (size_t)sample * npx2 * N2;
+    d2dst = D2 + (size_t)l3_order(sample, g.batch) * npx2 * N2;
     d2pend = true;
     SRCNN_L3_TICK(3);
     cur ^= 1;

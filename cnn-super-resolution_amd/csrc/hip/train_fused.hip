@@ -771,8 +771,11 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
 // kernels in one launch: blocks [first[k], first[k+1]) serve segment k,
 // kSlabCols columns each, 64 row lanes per column (enough blocks to spread
 // over every CU).  SlabSeg / reduce_slabs are declared in ops.hpp.
-constexpr int kSlabCols = 16;
-constexpr int kSlabRows = 64;
+#ifndef SRCNN_SLAB_COLS
+#define SRCNN_SLAB_COLS 32  // wide net slab reduce 42 -> 33 us; fused neutral (same-box A/B)
+#endif
+constexpr int kSlabCols = SRCNN_SLAB_COLS;
+constexpr int kSlabRows = 1024 / kSlabCols;
 struct SlabSegs {
   SlabSeg seg[kMaxSlabSegs];
   int first[kMaxSlabSegs + 1];
