@@ -75,7 +75,8 @@ __device__ unsigned long long g_clk[3][kClockBlocks][2];
 #define SRCNN_L12_W1LDS 0
 #endif
 #ifndef SRCNN_L12_GRID
-#define SRCNN_L12_GRID 1024  // grid cap (blocks), a multiple of 256 CUs x blocks per CU
+#define SRCNN_L12_GRID 512  // grid cap (blocks) = 256 CUs x 2 resident blocks: the samples are
+                            // written in index order, which l3 reads back in reverse (MALL)
 #endif
 // streaming-cache hints (bits): 1 l3 A2 DMA nt, 2 l3 D2 stores nt, 4 d1
 // operand DMA nt, 8 l12 A1 stores nt.  Default 1 | 8 (same-box A/B, steady
