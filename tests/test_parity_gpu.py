@@ -310,7 +310,10 @@ NETS = {"default": (64, 32, 9, 1, 5), "wide": (128, 64, 9, 5, 5), "tiny": (8, 4,
 
 @pytest.mark.parametrize("name,batch,size", [("default", 16, 33), ("wide", 3, 33), ("tiny", 5, 15),
                                              ("default", 2, 48), ("example", 7, 33),
-                                             ("default", 3, 21), ("default", 600, 33)])
+                                             ("default", 3, 21), ("default", 600, 33),
+                                             # ragged against the grids: l3 (256 blocks, walks the
+                                             # batch from its end), l12 / d1 (512 blocks)
+                                             ("default", 257, 33), ("default", 513, 33)])
 def test_train_step_vs_oracle(S, path, name, batch, size):
     cfg = NETS[name]
     net = S.Net(*cfg)
