@@ -85,6 +85,12 @@ KERNEL_STAGES = {
     "grad2_mfma": ["grad2"],
     "grad3": ["grad3"],
     "delta1_grad12_fused": ["delta1", "grad1", "grad2"],
+    # wide family (train_wide.hip)
+    "wide_l1_fwd": ["l1_fwd"],
+    "wide_l2_fwd": ["l2_fwd"],
+    "wide_l3_delta": ["l3_fwd", "last_delta", "delta2", "grad3"],
+    "wide_delta1_grad1": ["delta1", "grad1"],
+    "wide_grad2": ["grad2"],
 }
 
 
@@ -192,11 +198,23 @@ def synthetic_batch(rng, batch, w, h):
     return make_batch(rng, batch, w, h)
 
 
+def host_cores():
+    """CPU cores this process may run on, and the team size the baseline uses:
+    every core of the affinity mask, unless the host's OMP_NUM_THREADS says
+    otherwise (the GPU box sets it to the 16-core share of one GPU)."""
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        avail = os.cpu_count() or 1
+    want = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or avail
+    return avail, want
+
+
 def cpu_baseline(net, tiles_min=16, budget_s=12.0):
     """Time the CPU restatement of the reference path (oracle/, OpenMP) on a
     bounded sample of the same workload."""
     import srcnn_oracle as orc
-    want = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    avail, want = host_cores()
     threads = orc.set_threads(want)
     rng = np.random.default_rng(1234)
     batch = max(tiles_min, threads * 2)
@@ -215,9 +233,51 @@ def cpu_baseline(net, tiles_min=16, budget_s=12.0):
         el = time.perf_counter() - t0
         if el >= budget_s:
             break
-    return {"value": round(done / el, 2), "unit": "tiles/s", "cores": threads, "kind": "port",
+    return {"value": round(done / el, 2), "unit": "tiles/s", "cores": threads, "host_cpus": avail,
+            "kind": "port",
             "sample": "%d tiles of 33x33 (default net, fwd+bwd+update) in %.1fs with the oracle C "
                       "restatement (oracle/srcnn_oracle.c), OpenMP over tiles" % (done, el)}
+
+
+def forward_flops(net, w, h):
+    """Algorithmic FLOPs of the three layers over one w x h frame."""
+    n1, n2, f1, f2, f3 = net
+    w1, h1 = w - f1 + 1, h - f1 + 1
+    w2, h2 = w1 - f2 + 1, h1 - f2 + 1
+    w3, h3 = w2 - f3 + 1, h2 - f3 + 1
+    return 2.0 * (w1 * h1 * n1 * f1 * f1 + w2 * h2 * n2 * n1 * f2 * f2 + w3 * h3 * n2 * f3 * f3)
+
+
+def cpu_forward_baseline(net, strip_rows=48, reps=3):
+    """CPU restatement of the reference forward (oracle_forward, OpenMP over
+    output rows): BASELINE.json configs[0] (one 256x256 luma tile: ms and
+    GFLOP/s) and configs[4] measured on a bounded strip of the 3840x2160
+    frame (3840 x strip_rows input rows), reported as input Mpix/s."""
+    import srcnn_oracle as orc
+    avail, want = host_cores()
+    threads = orc.set_threads(want)
+    prm = init_params(net, orc.param_count(*net))
+    rng = np.random.default_rng(5)
+    out = {"cores": threads, "host_cpus": avail, "kind": "port"}
+    x = (rng.random(256 * 256, dtype=np.float32) - 0.5)
+    orc.forward(net, x, 256, 256, 1, prm)
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        orc.forward(net, x, 256, 256, 1, prm)
+        ts.append(time.perf_counter() - t0)
+    t = sorted(ts)[len(ts) // 2]
+    out["tile_256"] = {"ms": round(t * 1e3, 3), "gflop_s": round(forward_flops(net, 256, 256) / t / 1e9, 2),
+                       "sample": "median of %d forwards of one 256x256 tile (configs[0])" % reps}
+    x = (rng.random(3840 * strip_rows, dtype=np.float32) - 0.5)
+    t0 = time.perf_counter()
+    orc.forward(net, x, 3840, strip_rows, 1, prm)
+    t = time.perf_counter() - t0
+    out["frame_4k"] = {"mpix_s": round(3840 * strip_rows / t / 1e6, 3),
+                       "gflop_s": round(forward_flops(net, 3840, strip_rows) / t / 1e9, 2),
+                       "sample": "one 3840x%d strip of the 3840x2160 frame (configs[4]) in %.2fs"
+                                 % (strip_rows, t)}
+    return out
 
 
 def forward_4k(S, net_t, frames=5, warmup=2, w=3840, h=2160):
@@ -251,16 +311,23 @@ def forward_4k(S, net_t, frames=5, warmup=2, w=3840, h=2160):
     stats = S.profile_stats()
     ms = el / frames * 1e3
     # algorithmic work: the three layers over the frame
-    w1, h1 = w - f1 + 1, h - f1 + 1
-    w2, h2 = w1 - f2 + 1, h1 - f2 + 1
-    w3, h3 = w2 - f3 + 1, h2 - f3 + 1
-    flops = 2.0 * (w1 * h1 * n1 * f1 * f1 + w2 * h2 * n2 * n1 * f2 * f2 + w3 * h3 * n2 * f3 * f3)
+    flops = forward_flops(net_t, w, h)
     kernels = {k: {"launches_per_frame": c, "ms_per_frame": round(t, 4)} for k, (c, t) in stats.items()}
+    kname = "fwd_l123_mfma"
+    kroof = None
+    if kname in stats:
+        cnt, kms = stats[kname]
+        kdur = kms / cnt * 1e-3
+        ach = flops / kdur / 1e12  # the seam kernel's adds are ~0.01% of the frame's FLOPs
+        kroof = {"bound": "mfma", "achieved": round(ach, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                 "frac": round(ach / PEAK_FP32_TFLOPS, 4), "kernel": kname, "avg_launch_ms": round(kdur * 1e3, 5),
+                 "algorithmic_flops_per_launch": int(flops), "traffic": None}
     res = {"frame": "%dx%d" % (w, h), "frames": frames, "ms_per_frame": round(ms, 4),
            "mpix_s": round(w * h / (ms * 1e-3) / 1e6, 1),
            "tflops": round(flops / (ms * 1e-3) / 1e12, 2),
            "roofline_frac": round(flops / (ms * 1e-3) / 1e12 / PEAK_FP32_TFLOPS, 4),
-           "algorithmic_gflop_per_frame": round(flops / 1e9, 2), "kernels": kernels}
+           "algorithmic_gflop_per_frame": round(flops / 1e9, 2), "kernels": kernels,
+           "kernel_path": S.last_path(), "roofline": add_clock(kroof, held_clock(S, kname))}
     ghz = held_clock(S, "fwd_l123_mfma")
     if ghz:
         res["held_clock_ghz"] = round(ghz, 3)
@@ -314,12 +381,17 @@ def wide_training(S, steps=5, warmup=2, batch=4096):
     ms = el / steps * 1e3
     kernels = {k: {"launches_per_step": c / steps, "ms_per_step": round(t / steps, 4)}
                for k, (c, t) in stats.items()}
+    rooflines = {}
+    for k, (c, t) in stats.items():
+        r = roofline_of(k, c / steps, t / steps, work, batch, None, net_t, w, h)
+        if r:
+            rooflines[k] = r
     return {"workload": "SRCNN wide n1=128 n2=64 f1=9 f2=5 f3=5, fp32 training, 33x33 tiles, "
                         "batch %d (BASELINE.json configs[3])" % batch,
             "tiles_s": round(batch * steps / el, 1), "ms_per_step": round(ms, 4), "steps": steps,
             "tflops": round(flops / (ms * 1e-3) / 1e12, 2),
             "step_roofline": {"t_roof_ms": round(t_roof * 1e3, 4), "frac": round(t_roof * 1e3 / ms, 4)},
-            "kernels": kernels}
+            "kernel_path": S.last_path(), "kernels": kernels, "rooflines": rooflines}
 
 
 def main():
@@ -330,7 +402,11 @@ def main():
     # launches, flat over the next 275), so the default run warms up past it
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=30)
-    ap.add_argument("--batch", type=int, default=4096, help="tiles per GPU per step")
+    ap.add_argument("--batch", type=int, default=4096,
+                    help="tiles per GPU per step (weak scaling, the default line)")
+    ap.add_argument("--global-batch", type=int, default=None,
+                    help="strong scaling: this many tiles per step in total, sharded over the "
+                         "ranks (parallel.shard; SURVEY.md 8(d) config 3: 4096)")
     ap.add_argument("--path", choices=["auto", "generic"], default="auto")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-forward", action="store_true", help="skip the 4K inference line")
@@ -338,9 +414,15 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--profile-every", type=int, default=5,
                     help="per-kernel hipEvents on every N-th timed step (1 = every step)")
+    # N > 1: the gradient all-reduce is the library's own RCCL stage
+    # (srcnn_allreduce_grads over a srcnn_comm_init_rank communicator) by
+    # default; torch.distributed then only ships the RCCL id and runs the
+    # barriers / max-time reduction (gloo).  --comm torch uses dist.all_reduce.
+    ap.add_argument("--comm", choices=["srcnn", "torch"], default="srcnn")
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default=None,
+                    help="process-group backend (default: gloo with --comm srcnn, nccl with torch)")
     # rehearsal of the N>1 path on a single-GPU box (NOT a measurement):
     # every rank on one device, gradients all-reduced over gloo
-    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl")
     ap.add_argument("--all-ranks-on-device", type=int, default=None)
     args = ap.parse_args()
 
@@ -351,36 +433,46 @@ def main():
     dev_index = local if world > 1 else 0
     if args.all_ranks_on_device is not None:
         dev_index = args.all_ranks_on_device
+    backend = args.dist_backend or ("gloo" if args.comm == "srcnn" else "nccl")
     torch.cuda.set_device(dev_index)
-    parallel.init(args.dist_backend, torch.device("cuda", dev_index))
+    parallel.init(backend, torch.device("cuda", dev_index))
     S.set_path(0 if args.path == "auto" else 1)
     dev = torch.device("cuda", torch.cuda.current_device())
     stream = torch.cuda.current_stream().cuda_stream
 
     net_t = DEFAULT_NET
     net = S.Net(*net_t)
-    B, w, h = args.batch, TILE, TILE
+    strong = args.global_batch is not None
+    if strong:
+        _, B = parallel.shard(args.global_batch, rank, world)
+        global_tiles = args.global_batch
+    else:
+        B = args.batch
+        global_tiles = B * world
+    w, h = TILE, TILE
     P = S.net_param_count(net)
     rng = np.random.default_rng(1234 + rank)
-    X, T = synthetic_batch(rng, B, w, h)
+    X, T = synthetic_batch(rng, max(B, 1), w, h)
     prm = init_params(net_t, P)
     Xd = torch.from_numpy(X).to(dev)
     Td = torch.from_numpy(T).to(dev)
     params = torch.from_numpy(prm).to(dev)
     grads = torch.zeros(P, dtype=torch.float32, device=dev)
     mom = torch.zeros(P, dtype=torch.float32, device=dev)
-    ws_bytes = S.train_workspace_bytes(net, w, h, B)
+    ws_bytes = S.train_workspace_bytes(net, w, h, max(B, 1))
     ws = torch.empty(ws_bytes // 4 + 64, dtype=torch.float32, device=dev)
     lr = [1e-4, 1e-4, 1e-5]
-    global_tiles = B * world
 
+    comm = None
+    if world > 1 and args.comm == "srcnn":
+        comm = parallel.SrcnnComm(S, stream)
     # one rank's shard of the global batch -> grads; one all-reduce; the same
     # update on every rank (srcnn_amd/parallel.py)
     step = parallel.DataParallelStep(
         grads,
         lambda g: S.train_fwd_bwd(net, Xd, Td, w, h, B, params, g, None, ws, ws_bytes, stream),
         lambda nb: S.update_all(net, params, grads, mom, 0.9, 1e-3, lr, nb, stream),
-        global_tiles)
+        global_tiles, allreduce=comm)
 
     for _ in range(args.warmup):
         step()
@@ -409,8 +501,9 @@ def main():
     t1 = time.perf_counter()
     S.profile_enable(False)
     elapsed = t1 - t0
+    kernel_path = S.last_path()
     if world > 1:
-        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        e = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
     stats = S.profile_stats()
@@ -424,18 +517,29 @@ def main():
         kernels = {}
         for name, (cnt, ms) in stats.items():
             kernels[name] = {"launches_per_step": cnt / n_prof, "ms_per_step": round(ms / n_prof, 4)}
-        dominant = max(stats.items(), key=lambda kv: kv[1][1])[0] if stats else None
-        roof = None
-        if dominant:
-            cnt, ms = stats[dominant]
-            roof = add_clock(roofline_of(dominant, cnt / n_prof, ms / n_prof, work, B, pmc),
-                             held_clock(S, dominant))
+        rooflines = {}
+        for name, (cnt, ms) in stats.items():
+            r = roofline_of(name, cnt / n_prof, ms / n_prof, work, B, pmc)
+            if r:
+                rooflines[name] = add_clock(r, held_clock(S, name))
+        dominant = max(rooflines, key=lambda k: stats[k][1]) if rooflines else None
+        roof = rooflines.get(dominant)
         # whole-step roofline: T_roof = sum_stage max(F/peak, B/peak)
         t_roof = sum(max(f / (PEAK_FP32_TFLOPS * 1e12), b / (PEAK_HBM_GBS * 1e9))
                      for f, b in work.values()) * B
         ms_step = elapsed / K * 1e3
+        if strong:
+            metric = "training tiles/sec (fwd+bwd+update), default SRCNN 33x33, global batch %d" % global_tiles
+            workload = ("SRCNN default n1=64 n2=32 f1=9 f2=1 f3=5, fp32 training, 33x33 luma tiles, "
+                        "global batch %d sharded over %d GPUs (BASELINE.json configs[2], strong scaling)"
+                        % (global_tiles, world))
+        else:
+            metric = "training tiles/sec (fwd+bwd+update), default SRCNN 33x33, batch 4096/GPU"
+            workload = ("SRCNN default n1=64 n2=32 f1=9 f2=1 f3=5, fp32 training, 33x33 luma tiles, "
+                        "batch %d per GPU (BASELINE.json configs[1]%s)"
+                        % (B, ", configs[2] weak scaling" if world > 1 else ""))
         out = {
-            "metric": "training tiles/sec (fwd+bwd+update), default SRCNN 33x33, batch 4096/GPU",
+            "metric": metric,
             "value": round(value, 1),
             "unit": "tiles/s",
             "n_gpus": world,
@@ -443,15 +547,18 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (smooth random 33x33 luma patches, seed 1234+rank; weights N(0,1e-3))",
-            "config": {"workload": "SRCNN default n1=64 n2=32 f1=9 f2=1 f3=5, fp32 training, "
-                                   "33x33 luma tiles, batch 4096 per GPU (BASELINE.json configs[1])",
-                       "global_batch": global_tiles, "tile": "33x33", "parallelism": "dp%d" % world,
-                       "kernel_path": args.path},
+            "config": {"workload": workload, "global_batch": global_tiles, "batch_per_gpu": B,
+                       "tile": "33x33", "parallelism": "dp%d" % world,
+                       "kernel_path": kernel_path,
+                       "grad_allreduce": (("srcnn_allreduce_grads (RCCL)" if comm else
+                                           "torch.distributed all_reduce (%s)" % backend)
+                                          if world > 1 else None)},
             "roofline": roof,
+            "rooflines": rooflines,
             "step_roofline": {"t_roof_ms": round(t_roof * 1e3, 4), "frac": round(t_roof * 1e3 / ms_step, 4)},
             "kernels": kernels,
             "profiled_steps": n_prof,
@@ -463,7 +570,10 @@ def main():
             out["wide"] = wide_training(S)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(net_t, budget_s=args.cpu_budget)
+            out["cpu_forward_baseline"] = cpu_forward_baseline(net_t)
         print(json.dumps(out), flush=True)
+    if comm is not None:
+        comm.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -17,6 +17,22 @@ namespace {
 
 bool fast_enabled() { return srcnn::g_path == 0; }
 
+// kernel family of the most recent conv operator / network call (srcnn_last_path)
+thread_local const char* t_path = "";
+thread_local unsigned t_generic_ops = 0;  // op-level calls served by ops_generic.hip
+int tag(const char* path, int rc) {
+  if (rc == SRCNN_OK) {
+    t_path = path;
+    if (path[0] == 'g') ++t_generic_ops;
+  }
+  return rc;
+}
+// a network call composed of op-level calls: "generic" if any op was
+struct OpSequence {
+  unsigned g0 = t_generic_ops;
+  int done(int rc) { return tag(t_generic_ops != g0 ? "generic" : "fast", rc); }
+};
+
 int check_layer(const char* who, uint32_t n_prev, uint32_t n_cur, uint32_t f) {
   SRCNN_REQUIRE(f > 0 && n_prev > 0 && n_cur > 0,
                 "%s: f(%u), n_prev_filter_cnt(%u) and current_filter_count(%u) must be > 0", who,
@@ -67,6 +83,8 @@ size_t grad_ws_bytes(uint32_t n_prev, uint32_t n_cur, uint32_t f, uint32_t ow, u
 
 extern "C" {
 
+const char* srcnn_last_path(void) { return t_path; }
+
 int srcnn_fill_f32(float* dst, float value, size_t count, srcnn_stream_t stream) {
   if (count == 0) return SRCNN_OK;
   SRCNN_REQUIRE(dst, "srcnn_fill_f32: null pointer");
@@ -84,9 +102,10 @@ int srcnn_conv_fwd(const float* in, float* out, const float* W, const float* B, 
   hipStream_t s = as_stream(stream);
   if (fast_enabled()) {
     int rc = srcnn::fast::try_conv_fwd(in, out, W, B, in_w, in_h, n_prev, n_cur, f, relu, batch, s);
-    if (rc != 0) return rc < 0 ? rc : SRCNN_OK;
+    if (rc != 0) return rc < 0 ? rc : tag("fast", SRCNN_OK);
   }
-  return srcnn::generic::conv_fwd(in, out, W, B, in_w, in_h, n_prev, n_cur, f, relu, batch, s);
+  return tag("generic",
+             srcnn::generic::conv_fwd(in, out, W, B, in_w, in_h, n_prev, n_cur, f, relu, batch, s));
 }
 
 int srcnn_last_delta(const float* gt, const float* y, float* d, uint32_t gt_w, uint32_t gt_h,
@@ -112,10 +131,10 @@ int srcnn_conv_delta(const float* d_next, const float* y_curr, float* d_curr,
   if (fast_enabled()) {
     int rc = srcnn::fast::try_conv_delta(d_next, y_curr, d_curr, W_next, f_next, n_curr, n_next,
                                          curr_w, curr_h, batch, s);
-    if (rc != 0) return rc < 0 ? rc : SRCNN_OK;
+    if (rc != 0) return rc < 0 ? rc : tag("fast", SRCNN_OK);
   }
-  return srcnn::generic::conv_delta(d_next, y_curr, d_curr, W_next, f_next, n_curr, n_next,
-                                    curr_w, curr_h, batch, s);
+  return tag("generic", srcnn::generic::conv_delta(d_next, y_curr, d_curr, W_next, f_next, n_curr,
+                                                   n_next, curr_w, curr_h, batch, s));
 }
 
 size_t srcnn_conv_grad_workspace_bytes(uint32_t n_prev, uint32_t n_cur, uint32_t f,
@@ -137,10 +156,10 @@ int srcnn_conv_grad_acc(const float* in, const float* delta, float* gW, float* g
   if (fast_enabled()) {
     int rc = srcnn::fast::try_conv_grad_acc(in, delta, gW, gB, n_prev, n_cur, f, out_w, out_h,
                                             batch, ws, ws_bytes, s);
-    if (rc != 0) return rc < 0 ? rc : SRCNN_OK;
+    if (rc != 0) return rc < 0 ? rc : tag("fast", SRCNN_OK);
   }
-  return srcnn::generic::conv_grad_acc(in, delta, gW, gB, n_prev, n_cur, f, out_w, out_h, batch,
-                                       ws, ws_bytes, s);
+  return tag("generic", srcnn::generic::conv_grad_acc(in, delta, gW, gB, n_prev, n_cur, f, out_w,
+                                                      out_h, batch, ws, ws_bytes, s));
 }
 
 int srcnn_sgd_update(float* W, float* B, const float* gW, const float* gB, float* dW_prev,
@@ -292,12 +311,13 @@ int srcnn_train_fwd_bwd(const srcnn_net* net, const float* X, const float* T, ui
     rc = srcnn::fused::train_fwd_bwd(net, X, T, w, h, batch, params, grads, sq_err, A1, A2, D2,
                                      static_cast<float*>(gws), gws_bytes, srcnn::as_stream(stream),
                                      false, nullptr);
-    if (rc != 0) return rc < 0 ? rc : SRCNN_OK;
+    if (rc != 0) return rc < 0 ? rc : tag("fused", SRCNN_OK);
     rc = srcnn::wide::train_fwd_bwd(net, X, T, w, h, batch, params, grads, sq_err, A1, D1, A2, D2,
                                     static_cast<float*>(gws), gws_bytes, srcnn::as_stream(stream),
                                     false, nullptr);
-    if (rc != 0) return rc < 0 ? rc : SRCNN_OK;
+    if (rc != 0) return rc < 0 ? rc : tag("wide", SRCNN_OK);
   }
+  OpSequence seq;
   // forward: ConfigBasedDataPipeline.cpp:200-241
   if ((rc = srcnn_conv_fwd(X, A1, W1, B1, w, h, 1, net->n1, net->f1, 1, batch, stream))) return rc;
   if ((rc = srcnn_conv_fwd(A1, A2, W2, B2, d.w1, d.h1, net->n1, net->n2, net->f2, 1, batch, stream)))
@@ -320,8 +340,8 @@ int srcnn_train_fwd_bwd(const srcnn_net* net, const float* X, const float* T, ui
   if ((rc = srcnn_conv_grad_acc(A1, D2, gW2, gB2, net->n1, net->n2, net->f2, d.w2, d.h2, batch,
                                 gws, gws_bytes, stream)))
     return rc;
-  return srcnn_conv_grad_acc(X, D1, gW1, gB1, 1, net->n1, net->f1, d.w1, d.h1, batch, gws,
-                             gws_bytes, stream);
+  return seq.done(srcnn_conv_grad_acc(X, D1, gW1, gB1, 1, net->n1, net->f1, d.w1, d.h1, batch, gws,
+                                      gws_bytes, stream));
 }
 
 int srcnn_update_all(const srcnn_net* net, float* params, float* grads, float* momentum_bufs,
@@ -364,21 +384,22 @@ int srcnn_forward(const srcnn_net* net, const float* X, uint32_t w, uint32_t h, 
   if (fast_enabled()) {  // fused gfx950 inference (forward_fused.hip)
     int rc = srcnn::fused::forward(net, X, w, h, batch, params, out, ws, ws_bytes,
                                    as_stream(stream), false, nullptr);
-    if (rc != 0) return rc < 0 ? rc : SRCNN_OK;
+    if (rc != 0) return rc < 0 ? rc : tag("fused", SRCNN_OK);
   }
   size_t off[6];
   srcnn_net_offsets(net, off);
   float* A1 = static_cast<float*>(ws);
   float* A2 = reinterpret_cast<float*>(static_cast<char*>(ws) + align_up(d.s1 * batch * sizeof(float)));
   int rc;
+  OpSequence seq;
   if ((rc = srcnn_conv_fwd(X, A1, params + off[0], params + off[1], w, h, 1, net->n1, net->f1, 1,
                            batch, stream)))
     return rc;
   if ((rc = srcnn_conv_fwd(A1, A2, params + off[2], params + off[3], d.w1, d.h1, net->n1, net->n2,
                            net->f2, 1, batch, stream)))
     return rc;
-  return srcnn_conv_fwd(A2, out, params + off[4], params + off[5], d.w2, d.h2, net->n2, 1,
-                        net->f3, 0, batch, stream);
+  return seq.done(srcnn_conv_fwd(A2, out, params + off[4], params + off[5], d.w2, d.h2, net->n2, 1,
+                                 net->f3, 0, batch, stream));
 }
 
 }  // extern "C"

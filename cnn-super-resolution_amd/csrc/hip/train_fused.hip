@@ -834,14 +834,13 @@ static int grid_for_batch(uint32_t batch, int cap) { return (int)std::min<uint32
 template <int N2, int F3>
 static int launch_l3(const float* A2, const float* T, const float* W3, const float* B3, float* D2,
                      float* slab3, float* sqs, const L3Geom& lg, int grid, size_t lds, hipStream_t s) {
-  static bool attr = false;  // two A2 tiles exceed the 64 KiB default dynamic LDS
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)l3_delta_kernel<N2, F3>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (e != hipSuccess)
-      return fail(SRCNN_ERR_HIP, "hipFuncSetAttribute(l3_delta): %s", hipGetErrorString(e));
-    attr = true;
-  }
+  // two A2 tiles exceed the 64 KiB default dynamic LDS.  Set on every launch:
+  // the attribute is per device, and one process may drive several devices
+  // from several threads (cnn train --devices N)
+  hipError_t e = hipFuncSetAttribute((const void*)l3_delta_kernel<N2, F3>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (e != hipSuccess)
+    return fail(SRCNN_ERR_HIP, "hipFuncSetAttribute(l3_delta): %s", hipGetErrorString(e));
   hipLaunchKernelGGL((l3_delta_kernel<N2, F3>), dim3(grid), dim3(kL3Threads), lds, s, A2, T, W3,
                      B3, D2, slab3, sqs, lg);
   SRCNN_LAUNCH_TRY();

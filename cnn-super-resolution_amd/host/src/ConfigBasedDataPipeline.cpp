@@ -57,17 +57,24 @@ void ConfigBasedDataPipeline::init(int load_flags) {
 void ConfigBasedDataPipeline::load_kernels(int load_flags) {
   DataPipeline::load_kernels(load_flags);
   using srcnn::KernelKind;
+  // net-level launches carry the net shape as their defines
+  const std::string net_args = "-D N1=" + std::to_string(_config->n1) + " -D N2=" +
+                               std::to_string(_config->n2) + " -D F1=" + std::to_string(_config->f1) +
+                               " -D F2=" + std::to_string(_config->f2) + " -D F3=" +
+                               std::to_string(_config->f3);
   if ((load_flags & LOAD_KERNEL_LAYERS) && !_layer_1_kernel) {
     _layer_1_kernel = create_layer_kernel(layer_data_1, false);
     _layer_2_kernel = create_layer_kernel(layer_data_2, false);
     _layer_3_kernel = create_layer_kernel(layer_data_3, true);
-    _forward_kernel = _context->create_kernel(KernelKind::Layer, "forward(net)");
+    _forward_kernel = _context->create_kernel(KernelKind::Net, "srcnn_forward", 0, 0, 0, false, net_args);
   }
   if ((load_flags & LOAD_KERNEL_BACKPROPAGATE) && !_layer_1_deltas_kernel) {
     _layer_1_deltas_kernel = create_deltas_kernel(layer_data_1);
     _layer_2_deltas_kernel = create_deltas_kernel(layer_data_2);
-    _train_kernel = _context->create_kernel(KernelKind::Backprop, "train_fwd_bwd(net)");
-    _update_all_kernel = _context->create_kernel(KernelKind::Update, "update_all(net)");
+    _train_kernel = _context->create_kernel(KernelKind::Net, "srcnn_train_fwd_bwd", 0, 0, 0, false, net_args);
+    _update_all_kernel = _context->create_kernel(KernelKind::Net, "srcnn_update_all", 0, 0, 0, false, net_args);
+    _allreduce_kernel = _context->create_kernel(KernelKind::AllReduce, "srcnn_allreduce_grads", 0, 0, 0,
+                                                false, net_args);
   }
 }
 
@@ -293,6 +300,30 @@ void ConfigBasedDataPipeline::update_parameters(LayerAllocationPool& l1, LayerAl
   }
   _context->block();
   ++_epochs;
+}
+
+// ---------------------------------------------------------------- data parallel
+
+void ConfigBasedDataPipeline::allreduce_gradients(GpuAllocationPool& pools, srcnn_comm_t comm) {
+  check_initialized(LOAD_KERNEL_BACKPROPAGATE);
+  require(comm != nullptr, "allreduce_gradients: null communicator");
+  require(bind_flat(pools.layer_1, pools.layer_2, pools.layer_3),
+          "allreduce_gradients needs the pipeline's own (flat) parameter buffers");
+  srcnn_net nt = net();
+  srcnn::Context::Launch l(*_context, *_allreduce_kernel);
+  check(srcnn_allreduce_grads(comm, _context->fptr(_flat_grads), srcnn_net_param_count(&nt),
+                              _context->stream()),
+        "allreduce_gradients");
+}
+
+float ConfigBasedDataPipeline::allreduce_sum(float v, srcnn_comm_t comm) {
+  require(comm != nullptr, "allreduce_sum: null communicator");
+  if (_comm_scalar == gpu_nullptr) _comm_scalar = _context->allocate(srcnn::MEM_READ_WRITE, sizeof(float));
+  _context->write_buffer(_comm_scalar, &v, true);
+  check(srcnn_allreduce_grads(comm, _context->fptr(_comm_scalar), 1, _context->stream()), "allreduce_sum");
+  float out = 0.f;
+  _context->read_buffer(_comm_scalar, &out, true);
+  return out;
 }
 
 // ---------------------------------------------------------------- parameters I/O

@@ -88,6 +88,16 @@ class ConfigBasedDataPipeline : public DataPipeline {
   MemoryHandle flat_parameters() const { return _flat_params; }
   srcnn_net net() const;
 
+  /** Data-parallel extension (the reference is single-device): sum the
+   * flat gradient buffer over the ranks of `comm` in place, on this context's
+   * stream (srcnn_allreduce_grads, RCCL over xGMI).  Call between
+   * execute_batch(true, ...) on this rank's shard and update_parameters(...,
+   * global training-set size).  The pools must be the pipeline's own flat
+   * views (left unallocated by the caller; they are bound here if needed). */
+  void allreduce_gradients(GpuAllocationPool&, srcnn_comm_t comm);
+  /** sum of one host float over the ranks of `comm` (blocking) */
+  float allreduce_sum(float value, srcnn_comm_t comm);
+
  protected:
   void load_kernels(int load_flags) override;
 
@@ -132,6 +142,8 @@ class ConfigBasedDataPipeline : public DataPipeline {
   Kernel* _train_kernel = nullptr;
   Kernel* _forward_kernel = nullptr;
   Kernel* _update_all_kernel = nullptr;
+  Kernel* _allreduce_kernel = nullptr;
+  MemoryHandle _comm_scalar = gpu_nullptr;
 };
 
 }  // namespace cnn_sr

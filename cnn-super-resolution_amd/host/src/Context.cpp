@@ -31,16 +31,22 @@ void RawMemoryHandle::release() {
   released = true;
 }
 
-Kernel::Kernel(KernelKind k, std::string nm, size_t np, size_t nc, size_t ff, bool sr)
-    : kind(k), name(std::move(nm)), n_prev(np), n_cur(nc), f(ff), skip_relu(sr) {}
+Kernel::Kernel(KernelKind k, std::string nm, size_t np, size_t nc, size_t ff, bool sr,
+               std::string a)
+    : kind(k), name(std::move(nm)), n_prev(np), n_cur(nc), f(ff), skip_relu(sr), args(std::move(a)) {}
+
+std::string Kernel::compile_args() const {
+  // the defines of src/DataPipeline.cpp:161-180 (layer / deltas kernels)
+  if (kind == KernelKind::Layer && f > 0)
+    return "-D CURRENT_FILTER_COUNT=" + std::to_string(n_cur) + " -D PREVIOUS_FILTER_COUNT=" +
+           std::to_string(n_prev) + " -D F_SPATIAL_SIZE=" + std::to_string(f) +
+           (skip_relu ? " -D SKIP_RELU" : "");
+  if (kind == KernelKind::Deltas && n_cur > 0) return "-D CURRENT_FILTER_COUNT=" + std::to_string(n_cur);
+  return args.empty() ? "--" : args;
+}
 
 std::string Kernel::get_human_identifier() const {
-  std::string s = "'" + name + "'";
-  if (kind == KernelKind::Layer || kind == KernelKind::Deltas) {
-    s += " (n_prev=" + std::to_string(n_prev) + ", n=" + std::to_string(n_cur) +
-         ", f=" + std::to_string(f) + (skip_relu ? ", skip_relu" : "") + ")";
-  }
-  return s;
+  return "'gfx950/" + name + "'[" + compile_args() + "]";
 }
 
 uint64_t Kernel::get_total_execution_time() const {
@@ -231,8 +237,8 @@ Event Context::write_image(MemoryHandle h, const ImageData& img, bool blk, const
 }
 
 Kernel* Context::create_kernel(KernelKind kind, const std::string& name, size_t n_prev,
-                               size_t n_cur, size_t f, bool skip_relu) {
-  _kernels.emplace_back(new Kernel(kind, name, n_prev, n_cur, f, skip_relu));
+                               size_t n_cur, size_t f, bool skip_relu, const std::string& args) {
+  _kernels.emplace_back(new Kernel(kind, name, n_prev, n_cur, f, skip_relu, args));
   return _kernels.back().get();
 }
 

@@ -88,7 +88,9 @@ enum class KernelKind {
   Sum,          // sum.cl                -> srcnn_sum
   SubFromAll,   // subtract_from_all.cl  -> srcnn_sub_scalar
   Luma,         // extract_luma.cl       -> srcnn_extract_luma
-  SwapLuma      // swap_luma.cl          -> srcnn_swap_luma
+  SwapLuma,     // swap_luma.cl          -> srcnn_swap_luma
+  Net,          // (no .cl: fused net-level step) -> srcnn_train_fwd_bwd / srcnn_forward / srcnn_update_all
+  AllReduce     // (no reference kernel) -> srcnn_allreduce_grads (RCCL)
 };
 
 /**
@@ -101,14 +103,20 @@ enum class KernelKind {
 class Kernel {
  public:
   Kernel(KernelKind kind, std::string name, size_t n_prev = 0, size_t n_cur = 0,
-         size_t f = 0, bool skip_relu = false);
+         size_t f = 0, bool skip_relu = false, std::string args = "");
+  /** "'gfx950/<name>'[<args>]", the reference's "'<file>'[<-D args>]"
+   * (src/opencl/Kernel.cpp:32-36), so profile.py's regex parses the profile
+   * lines; args are the specialisation defines ("--" when there are none) */
   std::string get_human_identifier() const;
+  /** the -D defines the reference would have compiled this kernel with */
+  std::string compile_args() const;
   uint64_t get_total_execution_time() const;  // ns, profile mode only
 
   const KernelKind kind;
   const std::string name;
   const size_t n_prev, n_cur, f;
   const bool skip_relu;
+  const std::string args;
 
  private:
   friend class Context;
@@ -166,7 +174,8 @@ class Context {
 
   /** Kernel object owned by the context (reference create_kernel). */
   Kernel* create_kernel(KernelKind kind, const std::string& name, size_t n_prev = 0,
-                        size_t n_cur = 0, size_t f = 0, bool skip_relu = false);
+                        size_t n_cur = 0, size_t f = 0, bool skip_relu = false,
+                        const std::string& args = "");
   /** Bracket one launch of `k` (counts; device time when profiling). */
   class Launch {
    public:

@@ -38,14 +38,15 @@ void DataPipeline::load_kernels(int flags) {
   using srcnn::KernelKind;
   auto& c = *_context;
   if ((flags & LOAD_KERNEL_LUMA) && !_luma_kernel_norm) {
-    _luma_kernel_norm = c.create_kernel(KernelKind::Luma, "extract_luma(normalize)");
+    // names / defines of the reference's kernels (src/DataPipeline.cpp:121-159)
+    _luma_kernel_norm = c.create_kernel(KernelKind::Luma, "extract_luma", 0, 0, 0, false, "-D NORMALIZE");
     _luma_kernel_raw = c.create_kernel(KernelKind::Luma, "extract_luma");
     _swap_luma_kernel = c.create_kernel(KernelKind::SwapLuma, "swap_luma");
   }
   if ((flags & LOAD_KERNEL_MISC) && !_sum_kernel) {
     _squared_error_kernel = c.create_kernel(KernelKind::SquaredError, "squared_error");
     _sum_kernel = c.create_kernel(KernelKind::Sum, "sum");
-    _sum_squared_kernel = c.create_kernel(KernelKind::Sum, "sum(squared)");
+    _sum_squared_kernel = c.create_kernel(KernelKind::Sum, "sum", 0, 0, 0, false, "-D SUM_SQUARED");
     _subtract_from_all_kernel = c.create_kernel(KernelKind::SubFromAll, "subtract_from_all");
   }
   if ((flags & LOAD_KERNEL_BACKPROPAGATE) && !_backpropagate_kernel) {
@@ -109,7 +110,7 @@ void DataPipeline::print_buffer(MemoryHandle h, const char* name, size_t lines) 
 }
 
 Kernel* DataPipeline::create_layer_kernel(const LayerData& d, bool skip_relu) {
-  return _context->create_kernel(srcnn::KernelKind::Layer, "layer_forward", d.n_prev_filter_cnt,
+  return _context->create_kernel(srcnn::KernelKind::Layer, "layer_uber_kernel", d.n_prev_filter_cnt,
                                  d.current_filter_count, d.f_spatial_size, skip_relu);
 }
 

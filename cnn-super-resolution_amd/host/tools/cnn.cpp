@@ -2,7 +2,8 @@
 // pipeline:
 //
 //   cnn [-h] [train] [dry] [profile] -c CONFIG -i IN [-o OUT] [-e EPOCHS]
-//       [--seed N] [--device D] [--validation-percent P] [--mini-batches M]
+//       [--seed N] [--device D] [--devices N] [--validation-percent P]
+//       [--mini-batches M]
 //
 // forward:  IN is an image (PNG / PNM), OUT the upscaled result image
 // train:    IN is a directory of <name>_large.<ext> / <name>_small.<ext> pairs
@@ -12,7 +13,13 @@
 // (the reference hard-codes "\\", src/Main_cl.cpp:284-287), the epoch
 // shuffle is seeded (--seed; the reference uses unseeded rand()), JPEG is
 // not decoded (see host/src/Image.hpp).
+// Extension: `train --devices N` trains data-parallel on devices D .. D+N-1
+// of one node: one host thread per device, the epoch's training set sharded
+// contiguously over them, one RCCL all-reduce of the flat gradient buffer per
+// epoch (srcnn_allreduce_grads over ncclCommInitAll communicators), the same
+// update on every device.
 #include <dirent.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <cmath>
@@ -22,6 +29,7 @@
 #include <map>
 #include <random>
 #include <string>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -41,6 +49,8 @@ struct Args {
   uint64_t seed = 0;
   bool seeded = false;
   int device = 0;
+  int devices = 1;
+  bool devices_set = false;  // --devices given: the data-parallel driver (also for N = 1)
   size_t validation_percent = 20;  // src/Main_cl.cpp:87
   size_t mini_batches = 2;         // src/Main_cl.cpp:88
 };
@@ -48,7 +58,8 @@ struct Args {
 void usage() {
   std::cout
       << "usage: cnn [-h] [train] [dry] [profile] -c CONFIG -i IN [-o OUT] [-e EPOCHS]\n"
-         "           [--seed N] [--device D] [--validation-percent P] [--mini-batches M]\n\n"
+         "           [--seed N] [--device D] [--devices N] [--validation-percent P]\n"
+         "           [--mini-batches M]\n\n"
          "  -h, --help            print this help\n"
          "  train                 train mode\n"
          "  dry                   do not store the result\n"
@@ -59,6 +70,7 @@ void usage() {
          "  -e, --epochs EPOCHS   number of epochs during training\n"
          "  --seed N              seed of the random parameters and the epoch shuffles\n"
          "  --device D            HIP device index (default 0)\n"
+         "  --devices N           train data-parallel on devices D .. D+N-1 (default 1)\n"
          "  --validation-percent  share of samples used for validation (default 20)\n"
          "  --mini-batches M      mini-batches per epoch (default 2)\n";
 }
@@ -80,12 +92,14 @@ bool parse(int argc, char** argv, Args& a) {
     else if (s == "-e" || s == "--epochs") a.epochs = std::stoul(value("--epochs"));
     else if (s == "--seed") { a.seed = std::stoull(value("--seed")); a.seeded = true; }
     else if (s == "--device") a.device = std::stoi(value("--device"));
+    else if (s == "--devices") { a.devices = std::stoi(value("--devices")); a.devices_set = true; }
     else if (s == "--validation-percent") a.validation_percent = std::stoul(value("--validation-percent"));
     else if (s == "--mini-batches") a.mini_batches = std::stoul(value("--mini-batches"));
     else throw std::runtime_error("unknown argument '" + s + "'");
   }
   if (a.help) return false;
   if (a.config.empty() || a.in.empty()) throw std::runtime_error("--config and --in are required");
+  if (a.devices < 1) throw std::runtime_error("--devices must be >= 1");
   return true;
 }
 
@@ -142,17 +156,34 @@ int forward(ConfigBasedDataPipeline& p, const Args& a) {
   return 0;
 }
 
-int train(ConfigBasedDataPipeline& p, const Args& a) {
+/** Contiguous slice [start, start + count) of n items for `rank` of `world`
+ * (the remainder goes to the lowest ranks; srcnn_amd/parallel.py shard). */
+std::pair<size_t, size_t> shard(size_t n, int rank, int world) {
+  size_t base = n / world, rem = n % world, r = size_t(rank);
+  return {r * base + std::min(r, rem), base + (r < rem ? 1 : 0)};
+}
+
+/** One training run (src/Main_cl.cpp:157-195).  comm == nullptr: a single
+ * device.  Otherwise rank `rank` of a data-parallel run: every rank loads
+ * all samples and draws the same epoch split (same shuffle seed), trains on
+ * its shard of the training set, the gradients are all-reduced, and every
+ * rank applies the update with batch = |training set|. */
+int train(ConfigBasedDataPipeline& p, const Args& a, uint64_t shuffle_seed, srcnn_comm_t comm = nullptr,
+          int rank = 0, int world = 1) {
   auto& ctx = *p.context();
+  const bool lead = rank == 0;
   auto files = training_samples(a.in);
   if (files.empty()) throw std::runtime_error("no training samples in '" + a.in + "'");
   const size_t nval = files.size() * a.validation_percent / 100, ntrain = files.size() - nval;
-  if (nval == 0) std::cout << "[WARNING] Validation set is empty" << std::endl;
-  else
-    std::cout << "validation_set_size: " << nval << "/" << files.size() << " = "
-              << (nval * 100.0f / files.size()) << "%" << std::endl;
+  if (lead) {
+    if (nval == 0) std::cout << "[WARNING] Validation set is empty" << std::endl;
+    else
+      std::cout << "validation_set_size: " << nval << "/" << files.size() << " = "
+                << (nval * 100.0f / files.size()) << "%" << std::endl;
+  }
   srcnn::require(ntrain > 0, "Training set is empty");
-  p.set_mini_batch_size(ntrain / a.mini_batches + a.mini_batches);  // src/Main_cl.cpp:128-129
+  const size_t my_train = shard(ntrain, rank, world).second;
+  p.set_mini_batch_size(std::max<size_t>(my_train, 1) / a.mini_batches + a.mini_batches);  // src/Main_cl.cpp:128-129
 
   GpuAllocationPool pools;
   for (auto& f : files) {
@@ -172,7 +203,7 @@ int train(ConfigBasedDataPipeline& p, const Args& a) {
   }
   const size_t px = pools.samples[0].input_w * pools.samples[0].input_h;
 
-  std::mt19937_64 rng(a.seeded ? a.seed : std::random_device{}());
+  std::mt19937_64 rng(shuffle_seed);
   std::vector<size_t> order(pools.samples.size());
   bool error = false;
   for (size_t epoch = 0; epoch < a.epochs; ++epoch) {
@@ -182,27 +213,82 @@ int train(ConfigBasedDataPipeline& p, const Args& a) {
     std::vector<SampleAllocationPool*> val, tr;
     for (size_t i = 0; i < order.size(); ++i) (i < nval ? val : tr).push_back(&pools.samples[order[i]]);
 
-    p.execute_batch(true, pools, tr);
+    if (comm) {
+      auto sh = shard(tr.size(), rank, world);
+      std::vector<SampleAllocationPool*> mine(tr.begin() + sh.first, tr.begin() + sh.first + sh.second);
+      if (!mine.empty()) p.execute_batch(true, pools, mine);
+      p.allreduce_gradients(pools, comm);
+    } else {
+      p.execute_batch(true, pools, tr);
+    }
     p.update_parameters(pools.layer_1, pools.layer_2, pools.layer_3, tr.size());
 
     if (!val.empty() && (epoch % 25 == 0 || epoch == a.epochs - 1)) {
-      float err = p.execute_batch(false, pools, val);
+      float err;
+      if (comm) {
+        auto sh = shard(val.size(), rank, world);
+        std::vector<SampleAllocationPool*> mine(val.begin() + sh.first, val.begin() + sh.first + sh.second);
+        err = p.allreduce_sum(mine.empty() ? 0.f : p.execute_batch(false, pools, mine), comm);
+      } else {
+        err = p.execute_batch(false, pools, val);
+      }
       if (std::isnan(err)) {
-        std::cout << "Error: squared error is NAN, after " << epoch << "/" << a.epochs << " epochs"
-                  << std::endl;
+        if (lead)
+          std::cout << "Error: squared error is NAN, after " << epoch << "/" << a.epochs << " epochs"
+                    << std::endl;
         error = true;
         break;
       }
       float mean = err / val.size();
-      std::cout << "[" << epoch << "] mean validation error: " << mean << " (" << (mean / px)
-                << " per px)" << std::endl;
+      if (lead)
+        std::cout << "[" << epoch << "] mean validation error: " << mean << " (" << (mean / px)
+                  << " per px)" << std::endl;
     }
   }
-  if (!a.dry && !a.out.empty())
+  if (lead && !a.dry && !a.out.empty())
     p.write_params_to_file(a.out.c_str(), pools.layer_1, pools.layer_2, pools.layer_3);
   ctx.block();
-  std::cout << "DONE" << std::endl;
+  if (lead) std::cout << "DONE" << std::endl;
   return error ? 1 : 0;
+}
+
+/** `train --devices N`: one thread per device, each with its own Context
+ * (HIP device and stream) and pipeline over the same config and seed. */
+int train_data_parallel(const Config& cfg, const Args& a) {
+  const int n = a.devices;
+  std::vector<int> devs(n);
+  for (int i = 0; i < n; ++i) devs[i] = a.device + i;
+  std::vector<srcnn_comm_t> comms(n, nullptr);
+  srcnn::check(srcnn_comm_init_all(comms.data(), n, devs.data()), "srcnn_comm_init_all");
+  std::cout << "Data-parallel training on " << n << " devices (" << a.device << ".."
+            << (a.device + n - 1) << "), RCCL gradient all-reduce" << std::endl;
+  const uint64_t seed = a.seeded ? a.seed : std::random_device{}();
+  std::vector<int> rcs(n, 0);
+  std::vector<std::thread> threads;
+  for (int r = 0; r < n; ++r) {
+    threads.emplace_back([&, r]() {
+      try {
+        Config my_cfg = cfg;
+        srcnn::Context context;
+        context.init(a.profile && r == 0, devs[r]);
+        ConfigBasedDataPipeline pipeline(my_cfg, &context);
+        pipeline.set_random_seed(seed);  // identical initial replicas
+        pipeline.init(DataPipeline::LOAD_KERNEL_ALL);
+        rcs[r] = train(pipeline, a, seed, comms[r], r, n);
+      } catch (const std::exception& e) {
+        // the other ranks may be parked in a collective this one will never
+        // join: report and leave without unwinding them
+        std::cout << "[ERROR] rank " << r << ": " << e.what() << std::endl;
+        std::cout.flush();
+        _exit(1);
+      }
+    });
+  }
+  for (auto& t : threads) t.join();
+  for (auto c : comms) srcnn_comm_destroy(c);
+  int rc = 0;
+  for (int v : rcs) rc |= v;
+  return rc;
 }
 
 }  // namespace
@@ -237,6 +323,7 @@ int main(int argc, char** argv) {
     ConfigReader reader;
     Config cfg = reader.read(a.config.c_str());
     std::cout << cfg << std::endl;
+    if (a.train && a.devices_set) return train_data_parallel(cfg, a);
     srcnn::Context context;
     context.init(a.profile, a.device);
     int rc;
@@ -244,7 +331,7 @@ int main(int argc, char** argv) {
       ConfigBasedDataPipeline pipeline(cfg, &context);
       if (a.seeded) pipeline.set_random_seed(a.seed);
       pipeline.init(DataPipeline::LOAD_KERNEL_ALL);
-      rc = a.train ? train(pipeline, a) : forward(pipeline, a);
+      rc = a.train ? train(pipeline, a, a.seeded ? a.seed : std::random_device{}()) : forward(pipeline, a);
     }
     return rc;
   } catch (const std::exception& e) {

@@ -94,6 +94,15 @@ SIGNATURES = {
     "srcnn_profile_clock": (_I, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double)]),
     "srcnn_set_path": (_I, [_I]),
     "srcnn_get_path": (_I, []),
+    "srcnn_last_path": (ctypes.c_char_p, []),
+    "srcnn_comm_id": (_I, [ctypes.c_char_p]),
+    "srcnn_comm_init_rank": (_I, [ctypes.POINTER(_P), _I, ctypes.c_char_p, _I]),
+    "srcnn_comm_init_all": (_I, [ctypes.POINTER(_P), _I, ctypes.POINTER(_I)]),
+    "srcnn_comm_destroy": (_I, [_P]),
+    "srcnn_comm_rank": (_I, [_P, ctypes.POINTER(_I), ctypes.POINTER(_I)]),
+    "srcnn_comm_group_start": (_I, []),
+    "srcnn_comm_group_end": (_I, []),
+    "srcnn_allreduce_grads": (_I, [_P, _P, _S, _P]),
 }
 
 for _name, (_res, _args) in SIGNATURES.items():
@@ -108,7 +117,8 @@ class SrcnnError(RuntimeError):
         self.code = code
 
 
-OK, ERR_INVALID, ERR_HIP, ERR_WORKSPACE, ERR_ALLOC = 0, -1, -2, -3, -4
+OK, ERR_INVALID, ERR_HIP, ERR_WORKSPACE, ERR_ALLOC, ERR_COMM = 0, -1, -2, -3, -4, -5
+COMM_ID_BYTES = 128
 
 
 def _call(name, *args):
@@ -322,6 +332,53 @@ def set_path(p):
 
 def get_path():
     return _lib.srcnn_get_path()
+
+
+def last_path():
+    """Kernel family of this thread's most recent conv / network call:
+    "fused", "wide", "fast", "generic" or "" (srcnn_last_path)."""
+    return _lib.srcnn_last_path().decode()
+
+
+# ---- multi-GPU: RCCL gradient reduction (srcnn_comm_*, srcnn_allreduce_grads) ----
+def comm_id():
+    """128-byte RCCL unique id (ncclGetUniqueId), made on ONE rank."""
+    buf = ctypes.create_string_buffer(COMM_ID_BYTES)
+    _call("srcnn_comm_id", buf)
+    return buf.raw
+
+
+def comm_init_rank(nranks, uid, rank):
+    """Communicator of `rank` on the current device (one process per GPU)."""
+    if len(uid) != COMM_ID_BYTES:
+        raise ValueError("comm id must be %d bytes" % COMM_ID_BYTES)
+    c = _P()
+    _call("srcnn_comm_init_rank", ctypes.byref(c), nranks, uid, rank)
+    return c.value
+
+
+def comm_init_all(devices):
+    """One communicator per device of one process (ncclCommInitAll)."""
+    n = len(devices)
+    comms = (_P * n)()
+    devs = (_I * n)(*devices)
+    _call("srcnn_comm_init_all", comms, n, devs)
+    return list(comms)
+
+
+def comm_destroy(c):
+    _call("srcnn_comm_destroy", c)
+
+
+def comm_rank(c):
+    r, n = _I(), _I()
+    _call("srcnn_comm_rank", c, ctypes.byref(r), ctypes.byref(n))
+    return r.value, n.value
+
+
+def allreduce_grads(c, buf, count, s=None):
+    """In-place sum of `count` floats over all ranks, on stream `s`."""
+    _call("srcnn_allreduce_grads", c, ptr(buf), count, s)
 
 
 # ---- profiling (reference `profile` mode) ----

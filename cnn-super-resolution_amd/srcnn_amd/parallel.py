@@ -14,6 +14,14 @@ for N devices.
 Compute is injected (`fwd_bwd(grads)`, `update(batch)`): on a GPU these are
 `srcnn_amd.train_fwd_bwd` / `srcnn_amd.update_all` on the HIP stream the
 collective runs on; nothing here computes anything itself.
+
+The collective is injected too.  Two implementations:
+  SrcnnComm      the library's own RCCL stage (srcnn_comm_init_rank +
+                 srcnn_allreduce_grads, include/srcnn.h) on the compute stream;
+                 torch.distributed only ships the 128-byte RCCL id and runs
+                 the barriers (the default of bench.py)
+  torch          dist.all_reduce on the process group (RCCL with backend
+                 "nccl"; gloo in the CPU tests and the one-GPU rehearsal)
 """
 import os
 
@@ -48,11 +56,37 @@ def shard(global_batch, rank, world):
     return start, base + (1 if rank < rem else 0)
 
 
+class SrcnnComm:
+    """RCCL communicator of libsrcnn_hip.so for this rank (one process per
+    GPU): rank 0 makes the unique id (srcnn_comm_id), the process group
+    broadcasts it, every rank calls srcnn_comm_init_rank on its current
+    device.  `allreduce(buf, count)` = srcnn_allreduce_grads on `stream`."""
+
+    def __init__(self, S, stream=None, group=None):
+        self.S = S
+        self.stream = stream
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        box = [S.comm_id() if self.rank == 0 else None]
+        dist.broadcast_object_list(box, src=0, group=group)
+        self.comm = S.comm_init_rank(self.world, box[0], self.rank)
+
+    def __call__(self, grads):
+        self.S.allreduce_grads(self.comm, grads, grads.numel(), self.stream)
+
+    def close(self):
+        if self.comm:
+            self.S.comm_destroy(self.comm)
+            self.comm = None
+
+
 class DataParallelStep:
     """fwd_bwd(grads) accumulates this rank's gradients; update(global_batch)
-    applies the SGD step and zeroes the gradients (srcnn_update_all)."""
+    applies the SGD step and zeroes the gradients (srcnn_update_all).
+    `allreduce(grads)` sums the flat gradient buffer over ranks in place
+    (default: dist.all_reduce on `group`; SrcnnComm for the C-ABI stage)."""
 
-    def __init__(self, grads, fwd_bwd, update, global_batch, group=None):
+    def __init__(self, grads, fwd_bwd, update, global_batch, group=None, allreduce=None):
         if not isinstance(grads, torch.Tensor) or grads.dtype != torch.float32:
             raise TypeError("grads must be a float32 tensor (the flat gradient buffer)")
         self.grads = grads
@@ -61,10 +95,15 @@ class DataParallelStep:
         self.global_batch = int(global_batch)
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        self._allreduce = allreduce
 
     def allreduce(self):
         """Sum the flat gradient buffer over ranks (one collective per step)."""
-        if self.world > 1:
+        if self.world <= 1:
+            return
+        if self._allreduce is not None:
+            self._allreduce(self.grads)
+        else:
             dist.all_reduce(self.grads, op=dist.ReduceOp.SUM, group=self.group)
 
     def __call__(self):

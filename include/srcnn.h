@@ -43,7 +43,8 @@ enum {
   SRCNN_ERR_INVALID = -1,   /* bad shape / argument (reference: std::runtime_error) */
   SRCNN_ERR_HIP = -2,       /* HIP runtime failure (reference: check_error, Context.cpp:111-119) */
   SRCNN_ERR_WORKSPACE = -3, /* workspace smaller than the matching *_workspace_bytes() */
-  SRCNN_ERR_ALLOC = -4      /* device allocation failed */
+  SRCNN_ERR_ALLOC = -4,     /* device allocation failed */
+  SRCNN_ERR_COMM = -5       /* RCCL failure (multi-GPU gradient reduction) */
 };
 
 typedef void* srcnn_stream_t; /* hipStream_t */
@@ -225,6 +226,41 @@ SRCNN_API int srcnn_profile_clock(const char* kernel, double* ghz);
  * 0 = auto (fast specialisations where the shape matches), 1 = generic only. */
 SRCNN_API int srcnn_set_path(int path);
 SRCNN_API int srcnn_get_path(void);
+/* Kernel family that served the most recent operator / network call of this
+ * thread, so a slow path is never silent:
+ *   "fused"   train_fused.hip / forward_fused.hip (nets with f2 == 1)
+ *   "wide"    train_wide.hip (nets with a spatial middle layer)
+ *   "fast"    ops_fast.hip (gfx950 op-level specialisations)
+ *   "generic" ops_generic.hip (any shape; one thread per output)
+ *   ""        nothing launched yet on this thread */
+SRCNN_API const char* srcnn_last_path(void);
+
+/* ---- multi-GPU: the RCCL gradient-reduction stage ----
+ * The reference has one OpenCL queue and no multi-device path
+ * (src/Main_cl.cpp:157-195 runs execute_batch over the whole training set,
+ * then update_parameters).  Data-parallel training shards the tile batch:
+ * each device accumulates its shard's gradients into the flat
+ * [gW1|gB1|gW2|gB2|gW3|gB3] buffer (srcnn_train_fwd_bwd), ONE in-place
+ * all-reduce(SUM) over xGMI combines them (srcnn_allreduce_grads), and every
+ * device runs the same srcnn_update_all with batch = the global tile count. */
+typedef void* srcnn_comm_t; /* ncclComm_t */
+#define SRCNN_COMM_ID_BYTES 128
+/* ncclGetUniqueId: called on ONE rank, the bytes shipped to the others */
+SRCNN_API int srcnn_comm_id(uint8_t* id /* [SRCNN_COMM_ID_BYTES] */);
+/* one process per GPU: communicator of `rank` on the current device */
+SRCNN_API int srcnn_comm_init_rank(srcnn_comm_t* comm, int nranks, const uint8_t* id, int rank);
+/* one process driving `ndev` GPUs (devices = NULL: 0 .. ndev-1); comms[i]
+ * belongs to devices[i] and is used from the thread that drives it */
+SRCNN_API int srcnn_comm_init_all(srcnn_comm_t* comms, int ndev, const int* devices);
+SRCNN_API int srcnn_comm_destroy(srcnn_comm_t comm);
+SRCNN_API int srcnn_comm_rank(srcnn_comm_t comm, int* rank, int* nranks);
+/* ncclGroupStart / End: one thread issuing the collectives of several devices */
+SRCNN_API int srcnn_comm_group_start(void);
+SRCNN_API int srcnn_comm_group_end(void);
+/* in-place sum of `count` floats of `buf` over all ranks, enqueued on `stream`
+ * (ordered after the gradient kernels, before the update; no host sync) */
+SRCNN_API int srcnn_allreduce_grads(srcnn_comm_t comm, float* buf, size_t count,
+                                    srcnn_stream_t stream);
 
 #ifdef __cplusplus
 }

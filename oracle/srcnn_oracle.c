@@ -7,8 +7,8 @@
  * Each routine cites the reference file:line it restates.  Loop nests keep
  * the reference's per-work-item float accumulation order; outer loops are
  * reordered only where that leaves every accumulator's order unchanged
- * (noted inline).  OpenMP parallelises over samples, which never shares an
- * accumulator between threads.
+ * (noted inline).  OpenMP parallelises over samples (and over output rows
+ * in forward / deltas), which never shares an accumulator between threads.
  */
 #include "srcnn_oracle.h"
 
@@ -37,29 +37,35 @@ void oracle_conv_fwd(const float* in, float* out, const float* W,
                      const float* B, int in_w, int in_h, int n_prev,
                      int n_cur, int f, int relu, int batch) {
   const int out_w = in_w - f + 1, out_h = in_h - f + 1;  /* :48-49 */
-#pragma omp parallel for schedule(static)
-  for (int s = 0; s < batch; s++) {
+  /* One work item per output pixel (:43-56); the OpenMP team splits the
+   * (sample, row) pairs, so a single large frame (batch 1) uses every core
+   * and every accumulator keeps the reference's tap order. */
+#pragma omp parallel
+  {
     float* vals = (float*)malloc(sizeof(float) * (size_t)n_cur);
-    const float* img = in + (size_t)s * n_prev * in_w * in_h;      /* :51 */
-    float* dst = out + (size_t)s * n_cur * out_w * out_h;          /* :52 */
-    for (int y = 0; y < out_h; y++) {
-      for (int x = 0; x < out_w; x++) {
-        for (int n = 0; n < n_cur; n++) vals[n] = 0.0f;            /* :59-62 */
-        for (int dy = 0; dy < f; dy++) {                           /* :70 */
-          for (int dx = 0; dx < f; dx++) {                         /* :71 */
-            const float* px = img + ((size_t)(y + dy) * in_w + (x + dx)) * n_prev;
-            const float* w2d = W + (size_t)(dy * f + dx) * n_cur * n_prev;
-            for (int k = 0; k < n_prev; k++) {                     /* :76 */
-              const float v = px[k];
-              const float* w3d = w2d + (size_t)k * n_cur;
-              for (int n = 0; n < n_cur; n++) vals[n] += w3d[n] * v; /* :80-82 */
+#pragma omp for collapse(2) schedule(static)
+    for (int s = 0; s < batch; s++) {
+      for (int y = 0; y < out_h; y++) {
+        const float* img = in + (size_t)s * n_prev * in_w * in_h;    /* :51 */
+        float* dst = out + (size_t)s * n_cur * out_w * out_h;        /* :52 */
+        for (int x = 0; x < out_w; x++) {
+          for (int n = 0; n < n_cur; n++) vals[n] = 0.0f;            /* :59-62 */
+          for (int dy = 0; dy < f; dy++) {                           /* :70 */
+            for (int dx = 0; dx < f; dx++) {                         /* :71 */
+              const float* px = img + ((size_t)(y + dy) * in_w + (x + dx)) * n_prev;
+              const float* w2d = W + (size_t)(dy * f + dx) * n_cur * n_prev;
+              for (int k = 0; k < n_prev; k++) {                     /* :76 */
+                const float v = px[k];
+                const float* w3d = w2d + (size_t)k * n_cur;
+                for (int n = 0; n < n_cur; n++) vals[n] += w3d[n] * v; /* :80-82 */
+              }
             }
           }
-        }
-        float* o = dst + ((size_t)y * out_w + x) * n_cur;          /* :56 */
-        for (int n = 0; n < n_cur; n++) {                          /* :88-95 */
-          const float r = vals[n] + B[n];
-          o[n] = relu ? fmaxf(r, 0.0f) : r;
+          float* o = dst + ((size_t)y * out_w + x) * n_cur;          /* :56 */
+          for (int n = 0; n < n_cur; n++) {                          /* :88-95 */
+            const float r = vals[n] + B[n];
+            o[n] = relu ? fmaxf(r, 0.0f) : r;
+          }
         }
       }
     }
@@ -96,39 +102,43 @@ void oracle_conv_delta(const float* d_next, const float* y_curr,
                        int n_curr, int n_next, int curr_w, int curr_h,
                        int batch) {
   const int next_w = curr_w - f_next + 1, next_h = curr_h - f_next + 1; /* :56-57 */
-#pragma omp parallel for schedule(static)
-  for (int s = 0; s < batch; s++) {
+  /* (sample, row) pairs split over the OpenMP team, as in oracle_conv_fwd */
+#pragma omp parallel
+  {
     float* acc = (float*)malloc(sizeof(float) * (size_t)n_curr);
     float* deriv = (float*)malloc(sizeof(float) * (size_t)n_curr);
-    const float* yc = y_curr + (size_t)s * n_curr * curr_w * curr_h;  /* :59-60 */
-    const float* dn = d_next + (size_t)s * n_next * next_w * next_h;  /* :61-62 */
-    float* dc = d_curr + (size_t)s * n_curr * curr_w * curr_h;
-    for (int y = 0; y < curr_h; y++) {
-      for (int x = 0; x < curr_w; x++) {
-        const size_t idx = ((size_t)y * curr_w + x) * n_curr;        /* :55 */
-        for (int n = 0; n < n_curr; n++) {                           /* :72-77 */
-          acc[n] = 0.0f;
-          deriv[n] = yc[idx + n] > 0.0f ? 1.0f : 0.0f;
-        }
-        for (int dy = 0; dy < f_next; dy++) {                        /* :79 */
-          for (int dx = 0; dx < f_next; dx++) {                      /* :80 */
-            const int nx = x - dx, ny = y - dy;                      /* :82 */
-            const int in_range = nx >= 0 && nx < next_w && ny >= 0 && ny < next_h; /* :94-96 */
-            /* out-of-range terms add (0*w)*deriv == 0: skipping them
-             * leaves every accumulator unchanged. */
-            if (!in_range) continue;
-            const size_t w2d = (size_t)(dy * f_next + dx) * n_next * n_curr; /* :83-84 */
-            const float* dptr = dn + ((size_t)ny * next_w + nx) * n_next;     /* :91-93 */
-            for (int k = 0; k < n_next; k++) {                       /* :86 */
-              const float delta = dptr[k];                           /* :97-100 */
-              for (int n = 0; n < n_curr; n++) {                     /* :102 */
-                const float w = W_next[w2d + (size_t)n * n_next + k]; /* :105-106 */
-                acc[n] += delta * w * deriv[n];                      /* :112 */
+#pragma omp for collapse(2) schedule(static)
+    for (int s = 0; s < batch; s++) {
+      for (int y = 0; y < curr_h; y++) {
+        const float* yc = y_curr + (size_t)s * n_curr * curr_w * curr_h;  /* :59-60 */
+        const float* dn = d_next + (size_t)s * n_next * next_w * next_h;  /* :61-62 */
+        float* dc = d_curr + (size_t)s * n_curr * curr_w * curr_h;
+        for (int x = 0; x < curr_w; x++) {
+          const size_t idx = ((size_t)y * curr_w + x) * n_curr;        /* :55 */
+          for (int n = 0; n < n_curr; n++) {                           /* :72-77 */
+            acc[n] = 0.0f;
+            deriv[n] = yc[idx + n] > 0.0f ? 1.0f : 0.0f;
+          }
+          for (int dy = 0; dy < f_next; dy++) {                        /* :79 */
+            for (int dx = 0; dx < f_next; dx++) {                      /* :80 */
+              const int nx = x - dx, ny = y - dy;                      /* :82 */
+              const int in_range = nx >= 0 && nx < next_w && ny >= 0 && ny < next_h; /* :94-96 */
+              /* out-of-range terms add (0*w)*deriv == 0: skipping them
+               * leaves every accumulator unchanged. */
+              if (!in_range) continue;
+              const size_t w2d = (size_t)(dy * f_next + dx) * n_next * n_curr; /* :83-84 */
+              const float* dptr = dn + ((size_t)ny * next_w + nx) * n_next;     /* :91-93 */
+              for (int k = 0; k < n_next; k++) {                       /* :86 */
+                const float delta = dptr[k];                           /* :97-100 */
+                for (int n = 0; n < n_curr; n++) {                     /* :102 */
+                  const float w = W_next[w2d + (size_t)n * n_next + k]; /* :105-106 */
+                  acc[n] += delta * w * deriv[n];                      /* :112 */
+                }
               }
             }
           }
+          for (int n = 0; n < n_curr; n++) dc[idx + n] = acc[n];       /* :121-123 */
         }
-        for (int n = 0; n < n_curr; n++) dc[idx + n] = acc[n];       /* :121-123 */
       }
     }
     free(acc);

@@ -87,3 +87,58 @@ def test_cli_train_then_forward(tmp_path):
     assert p.returncode == 0, p.stdout
     res = Image.open(out)
     assert res.size == (64, 48) and res.mode == "RGB"
+
+
+# the reference's profile.py regex (profile.py:9), verbatim as data
+PROFILE_REGEX = r"Kernel '.*/(.*?]).*?([\-e.\d]+)ns.*?([\-e.\d]+)s"
+
+
+def _train_args(tmp_path, samples, out, *extra):
+    cfg = tmp_path / "config.json"
+    if not cfg.exists():
+        write_config(cfg)
+    return ("train", "-c", str(cfg), "-i", str(samples), "-o", str(out), "-e", "5", "--seed", "3",
+            *extra)
+
+
+@pytest.mark.gpu
+def test_cli_devices_one_rank_matches_single_device(tmp_path):
+    """`train --devices 1` runs the data-parallel driver (thread per device,
+    ncclCommInitAll, RCCL all-reduce of the flat gradients, sharded
+    validation + scalar all-reduce) on one rank: it must produce exactly the
+    parameters of the plain single-device run."""
+    samples = tmp_path / "samples"
+    subprocess.check_call([sys.executable, MAKE_SAMPLES, "--synthetic", "5", "--per-image", "4",
+                           "-o", str(samples), "-s", "33", "--seed", "4"])
+    a, b = tmp_path / "single.json", tmp_path / "dp.json"
+    p = cnn(*_train_args(tmp_path, samples, a))
+    assert p.returncode == 0, p.stdout
+    p = cnn(*_train_args(tmp_path, samples, b, "--devices", "1"))
+    print(p.stdout[-2000:])
+    assert p.returncode == 0, p.stdout
+    assert "Data-parallel training on 1 devices" in p.stdout and "DONE" in p.stdout
+    assert json.load(open(a)) == json.load(open(b))
+
+
+@pytest.mark.gpu
+def test_cli_profile_output_parses_with_reference_regex(tmp_path):
+    """`cnn profile` prints one line per kernel in the reference's format
+    "Kernel '<dir>/<file>'[<defines>] total execution time: Nns = Ss"
+    (src/opencl/Kernel.cpp:32-36, src/opencl/Context.cpp:88-96), which the
+    reference's profile.py parses (profile.py:9-18)."""
+    import re
+    samples = tmp_path / "samples"
+    subprocess.check_call([sys.executable, MAKE_SAMPLES, "--synthetic", "3", "--per-image", "4",
+                           "-o", str(samples), "-s", "33", "--seed", "5"])
+    p = cnn("profile", *_train_args(tmp_path, samples, tmp_path / "p.json"))
+    assert p.returncode == 0, p.stdout
+    found = re.findall(PROFILE_REGEX, p.stdout)
+    names = {x[0] for x in found}
+    print(sorted(names))
+    assert "srcnn_train_fwd_bwd'[-D N1=64 -D N2=32 -D F1=9 -D F2=1 -D F3=5]" in names
+    assert "srcnn_update_all'[-D N1=64 -D N2=32 -D F1=9 -D F2=1 -D F3=5]" in names
+    assert "extract_luma'[-D NORMALIZE]" in names
+    for name, ns, s in found:
+        assert int(ns) >= 0 and abs(float(s) - int(ns) / 1e9) <= 1e-6 + 1e-3 * float(s)
+    train = [x for x in found if x[0].startswith("srcnn_train_fwd_bwd")][0]
+    assert int(train[1]) > 0  # device time was recorded

@@ -1,0 +1,141 @@
+"""Data-parallel training of the HIP path on the GPU.
+
+- world_size 2: two rank processes on device 0 run the HIP training step
+  under srcnn_amd.parallel.DataParallelStep on their shards of one global
+  batch.  The replicas must be bit-identical, and equal (1e-4 rel) to one
+  process training the union batch, both on the HIP path and in the oracle.
+- the RCCL stage of the C ABI (srcnn_comm_*, srcnn_allreduce_grads) on a
+  one-rank communicator: ncclCommInitAll and ncclCommInitRank, the in-place
+  sum on the compute stream (the 8-GPU all-reduce is bench.py's, run by the
+  driver on a whole node).
+"""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import srcnn_oracle as orc
+from conftest import ROOT
+from hip_util import assert_close, make_batch, make_params
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+LR = [1e-4, 1e-4, 1e-5]
+
+
+@pytest.fixture(scope="module")
+def S():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import srcnn_amd
+    return srcnn_amd
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _union_hip(S, net_t, gb, steps, tile):
+    rng = np.random.default_rng(2024)
+    X, T = make_batch(rng, gb, tile, tile)
+    p0 = make_params(rng, net_t, sd=0.05)
+    net = S.Net(*net_t)
+    P = S.net_param_count(net)
+    dev = torch.device("cuda", 0)
+    Xd, Td = torch.from_numpy(X).to(dev), torch.from_numpy(T).to(dev)
+    params = torch.from_numpy(p0.copy()).to(dev)
+    grads = torch.zeros(P, device=dev)
+    mom = torch.zeros(P, device=dev)
+    nbytes = S.train_workspace_bytes(net, tile, tile, gb)
+    ws = torch.empty(nbytes // 4 + 64, device=dev)
+    for _ in range(steps):
+        S.train_fwd_bwd(net, Xd, Td, tile, tile, gb, params, grads, None, ws, nbytes)
+        S.update_all(net, params, grads, mom, 0.9, 1e-3, LR, gb)
+    torch.cuda.synchronize()
+    return p0, params.cpu().numpy(), X, T
+
+
+def _union_oracle(net_t, X, T, p0, gb, steps, tile):
+    p, g, m = p0.copy(), np.zeros_like(p0), np.zeros_like(p0)
+    for _ in range(steps):
+        g, _ = orc.train_fwd_bwd(net_t, X, T, tile, tile, gb, p, g)
+        p, g, m = orc.update_all(net_t, p, g, m, 0.9, 1e-3, LR, gb)
+    return p
+
+
+@pytest.mark.parametrize("net_t,gb,tile,want", [
+    ((64, 32, 9, 1, 5), 96, 33, "fused"),     # default net, fused kernels
+    ((64, 32, 9, 1, 5), 7, 21, "fused"),      # odd batch: ranks get 4 and 3 tiles
+    ((16, 8, 5, 3, 3), 10, 19, "generic"),   # spatial middle layer, op-level path
+], ids=["default", "ragged", "spatial"])
+def test_two_ranks_match_union_batch(S, tmp_path, net_t, gb, tile, want):
+    steps, world = 2, 2
+    port = _free_port()
+    worker = os.path.join(ROOT, "tests", "dp_worker.py")
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(
+            [sys.executable, worker, str(tmp_path), ",".join(map(str, net_t)), str(gb), str(steps),
+             str(tile)], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
+    for p in procs:
+        out, _ = p.communicate(timeout=240)
+        assert p.returncode == 0, out.decode()[-3000:]
+    reps = [np.load(tmp_path / ("params_%d.npy" % r)) for r in range(world)]
+    assert np.array_equal(reps[0], reps[1]), "replicas diverged"
+    for r in range(world):
+        paths = (tmp_path / ("path_%d.txt" % r)).read_text().split(",")
+        assert set(paths) == {want}, paths
+    p0, hip_union, X, T = _union_hip(S, net_t, gb, steps, tile)
+    ref = _union_oracle(net_t, X, T, p0, gb, steps, tile)
+    # the update moves the parameters by ~lr*g/batch: compare the movement
+    assert not np.array_equal(reps[0], p0)
+    assert_close(reps[0] - p0, ref - p0, what="2-rank step vs oracle union batch")
+    assert_close(reps[0] - p0, hip_union - p0, what="2-rank step vs HIP union batch")
+
+
+def _check_identity_allreduce(S, comm):
+    dev = torch.device("cuda", 0)
+    v = torch.arange(8129, dtype=torch.float32, device=dev) * 0.5 - 7.0
+    want = v.cpu().numpy()
+    stream = torch.cuda.current_stream().cuda_stream
+    S.allreduce_grads(comm, v, v.numel(), stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(v.cpu().numpy(), want)  # one rank: the sum is the buffer itself
+
+
+def test_rccl_comm_init_all_one_device(S):
+    comms = S.comm_init_all([0])
+    try:
+        assert S.comm_rank(comms[0]) == (0, 1)
+        _check_identity_allreduce(S, comms[0])
+    finally:
+        S.comm_destroy(comms[0])
+
+
+def test_rccl_comm_init_rank_one_rank(S):
+    uid = S.comm_id()
+    assert len(uid) == S.COMM_ID_BYTES
+    c = S.comm_init_rank(1, uid, 0)
+    try:
+        assert S.comm_rank(c) == (0, 1)
+        _check_identity_allreduce(S, c)
+    finally:
+        S.comm_destroy(c)
+
+
+def test_rccl_invalid_arguments(S):
+    with pytest.raises(S.SrcnnError):
+        S.comm_init_rank(2, S.comm_id(), 5)
+    with pytest.raises(S.SrcnnError):
+        S.comm_init_all([S.device_count()])
+    with pytest.raises(S.SrcnnError):
+        S.allreduce_grads(None, 0, 4)
