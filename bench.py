@@ -248,7 +248,7 @@ def forward_flops(net, w, h):
     return 2.0 * (w1 * h1 * n1 * f1 * f1 + w2 * h2 * n2 * n1 * f2 * f2 + w3 * h3 * n2 * f3 * f3)
 
 
-def cpu_forward_baseline(net, strip_rows=48, reps=3):
+def cpu_forward_baseline(net, strip_rows=256, reps=3):
     """CPU restatement of the reference forward (oracle_forward, OpenMP over
     output rows): BASELINE.json configs[0] (one 256x256 luma tile: ms and
     GFLOP/s) and configs[4] measured on a bounded strip of the 3840x2160

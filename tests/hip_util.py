@@ -1,10 +1,39 @@
 """Helpers shared by the GPU tests: device buffers (torch, plumbing only),
 tolerance checks, synthetic SRCNN inputs."""
+import json
+import os
+
 import numpy as np
 
-# Normwise fp32 tolerance of BASELINE.json's north_star ("outputs within 1e-4
-# rel of the reference"): every element within 1e-4 x (|ref| + max|ref|).
+# fp32 tolerance of BASELINE.json's north_star ("outputs within 1e-4 rel of
+# the reference"), checked two ways by assert_close:
+#   normwise     every element within RTOL x (|ref| + max|ref|) of the fp32
+#                oracle (the reference's loop nests and accumulation order)
+#   elementwise  on every SIGNIFICANT element (|exact| >= SIG x max|exact|),
+#                the relative error against the exact result -- the oracle's
+#                double-precision build (oracle/srcnn_oracle_f64.c) -- must be
+#                <= RTOL, or, where the reference's own fp32 algorithm is
+#                further off than that, no worse than K_REF x the fp32
+#                oracle's own relative error there
+# The second clause is for sums that cancel: a gradient element made of a few
+# thousand terms can come out 1000x smaller than its terms, and there any two
+# fp32 summation orders (the reference's sample-serial loop, the HIP path's
+# blocked sums) differ by far more than 1e-4 of the element.
+# Gradients add an absolute floor of FLIP_FLOOR x max|exact|: a ReLU decision
+# whose pre-activation lies within fp32 rounding of zero can go either way in
+# any fp32 order, and the whole delta of that element then enters (or leaves)
+# the weight gradients.  Measured (tools/debug/mask_flips.py, default net,
+# 600 tiles): 1 of 24M A1 elements came out +1.9e-9 where the exact value is
+# 0; its delta1 (0.2 x max|delta1|) moved gW1 by 1.2e-5 x max|gW1|, i.e. 7.8e-4
+# relative on elements near 1e-3 x max, in BOTH HIP paths (fused and generic).
+# Measured, not assumed: tests report every error (SRCNN_PARITY_LOG).
 RTOL = 1e-4
+SIG = 1e-3
+K_REF = 4.0
+FLIP_FLOOR = 2e-5
+# SRCNN_PARITY_LOG=<file>: append one JSON line per check with the achieved
+# normwise and elementwise errors (the GPU sessions collect them)
+PARITY_LOG = os.environ.get("SRCNN_PARITY_LOG")
 
 
 def dev(a, torch):
@@ -25,13 +54,52 @@ def max_rel_err(got, ref):
     return float((np.abs(got - ref) / (np.abs(ref) + scale)).max())
 
 
-def assert_close(got, ref, rtol=RTOL, what=""):
+def max_elem_rel_err(got, exact, sig=SIG):
+    """(max |g - x| / |x| over elements with |x| >= sig * max|x|, count)."""
+    got = np.asarray(got, np.float64).ravel()
+    exact = np.asarray(exact, np.float64).ravel()
+    if exact.size == 0:
+        return 0.0, 0
+    a = np.abs(exact)
+    if a.max() == 0:
+        return 0.0, 0
+    m = a >= sig * a.max()
+    return float((np.abs(got[m] - exact[m]) / a[m]).max()), int(m.sum())
+
+
+def assert_close(got, ref, rtol=RTOL, what="", ref64=None, abs_floor=0.0):
+    """Normwise check against the fp32 oracle `ref`; with `ref64` (the same
+    computation by the double-precision oracle) also the elementwise check
+    described at RTOL, each element allowed abs_floor x max|ref64| on top
+    (FLIP_FLOOR for gradients).  Returns the normwise error."""
     got = np.asarray(got)
     ref = np.asarray(ref)
     assert got.shape == ref.shape, (what, got.shape, ref.shape)
     assert np.all(np.isfinite(got)), what + ": non-finite values"
     err = max_rel_err(got, ref)
+    rec = {"what": what, "n": int(ref.size), "normwise": err, "rtol": rtol}
+    el = el_ref = None
+    if ref64 is not None:
+        ref64 = np.asarray(ref64)
+        assert ref64.shape == ref.shape, (what, ref64.shape, ref.shape)
+        el, n_sig = max_elem_rel_err(got, ref64)
+        el_ref, _ = max_elem_rel_err(ref, ref64)
+        bound = max(rtol, K_REF * el_ref)
+        x = np.abs(np.asarray(ref64, np.float64).ravel())
+        sig = x >= SIG * x.max() if x.size and x.max() > 0 else np.zeros(x.size, bool)
+        over = np.abs(np.asarray(got, np.float64).ravel() - np.asarray(ref64, np.float64).ravel()) \
+            - bound * x - abs_floor * (x.max() if x.size else 0.0)
+        n_over = int((over[sig] > 0).sum())
+        rec.update(elementwise=el, elementwise_fp32_oracle=el_ref, significant=n_sig,
+                   abs_floor=abs_floor, n_over=n_over)
+    if PARITY_LOG:
+        with open(PARITY_LOG, "a") as fh:
+            fh.write(json.dumps(rec) + "\n")
     assert err <= rtol, "%s: max normwise rel err %.3e > %.1e" % (what, err, rtol)
+    if el is not None:
+        assert n_over == 0, ("%s: %d of %d significant elements off the exact result by more than "
+                             "%.2e rel + %.1e x max (max rel err %.3e; fp32 oracle's own %.3e)"
+                             % (what, n_over, n_sig, bound, abs_floor, el, el_ref))
     return err
 
 

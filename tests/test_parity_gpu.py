@@ -15,7 +15,7 @@ import pytest
 
 import srcnn_oracle as orc
 from conftest import GOLDEN
-from hip_util import RTOL, assert_close, make_batch, make_params
+from hip_util import FLIP_FLOOR, RTOL, assert_close, make_batch, make_params
 
 pytestmark = pytest.mark.gpu
 
@@ -104,8 +104,10 @@ def test_backpropagation_big_data(S, path):
     S.conv_grad_acc(D(inp), D(dl), gW, gB, n_prev, n_cur, f, ow, ow, 1, ws, nbytes)
     rW, rB = orc.conv_grad_acc(inp, dl, np.zeros(f * f * n_prev * n_cur), np.zeros(n_cur), n_prev,
                                n_cur, f, ow, ow, 1)
-    assert_close(H(gW), rW, 2e-4, "gW big data")   # 1M-term fp32 sums
-    assert_close(H(gB), rB, 2e-4, "gB big data")
+    xW, xB = orc.f64.conv_grad_acc(inp, dl, np.zeros(f * f * n_prev * n_cur), np.zeros(n_cur), n_prev,
+                                   n_cur, f, ow, ow, 1)
+    assert_close(H(gW), rW, 2e-4, "gW big data", xW)   # 1M-term fp32 sums
+    assert_close(H(gB), rB, 2e-4, "gB big data", xB)
 
 
 def test_update_parameters_spec(S):
@@ -245,7 +247,7 @@ def test_conv_fwd_vs_oracle(S, path, shape):
     ref = orc.conv_fwd(x, W, B, iw, ih, n_prev, n_cur, f, relu, b)
     out = zeros(ref.size)
     S.conv_fwd(D(x), out, D(W), D(B), iw, ih, n_prev, n_cur, f, relu, b)
-    assert_close(H(out), ref, RTOL, "conv_fwd")
+    assert_close(H(out), ref, RTOL, "conv_fwd", orc.f64.conv_fwd(x, W, B, iw, ih, n_prev, n_cur, f, relu, b))
 
 
 DELTA_SHAPES = [
@@ -270,7 +272,8 @@ def test_conv_delta_vs_oracle(S, path, shape):
     ref = orc.conv_delta(d_next, y, W, f, n_curr, n_next, cw, ch, b)
     out = zeros(ref.size)
     S.conv_delta(D(d_next), D(y), out, D(W), f, n_curr, n_next, cw, ch, b)
-    assert_close(H(out), ref, RTOL, "conv_delta")
+    assert_close(H(out), ref, RTOL, "conv_delta",
+                 orc.f64.conv_delta(d_next, y, W, f, n_curr, n_next, cw, ch, b))
 
 
 GRAD_SHAPES = [
@@ -297,8 +300,9 @@ def test_conv_grad_vs_oracle(S, path, shape):
     ws = zeros(nbytes // 4 + 1)
     gW, gB = D(gW0), D(gB0)
     S.conv_grad_acc(D(inp), D(dl), gW, gB, n_prev, n_cur, f, ow, oh, b, ws, nbytes)
-    assert_close(H(gW), rW, RTOL, "gW")
-    assert_close(H(gB), rB, RTOL, "gB")
+    xW, xB = orc.f64.conv_grad_acc(inp, dl, gW0, gB0, n_prev, n_cur, f, ow, oh, b)
+    assert_close(H(gW), rW, RTOL, "gW", xW)
+    assert_close(H(gB), rB, RTOL, "gB", xB)
 
 
 # ----------------------------------------------------------------------------
@@ -308,12 +312,27 @@ NETS = {"default": (64, 32, 9, 1, 5), "wide": (128, 64, 9, 5, 5), "tiny": (8, 4,
         "example": (32, 16, 9, 1, 5)}
 
 
+def expected_train_path(name, size, path):
+    """Kernel family srcnn_train_fwd_bwd must report (srcnn_last_path): the
+    fused f2 == 1 kernels take tiles whose A2 (two ping-pong copies in l3's
+    160 KB LDS) has at most 640 pixels, i.e. up to 33x33 for f1 = 9."""
+    if path == 1:
+        return {"generic"}
+    if name in ("default", "example") and (size - 8) ** 2 <= 640:
+        return {"fused"}
+    if name == "wide":
+        return {"wide"}
+    return {"generic", "fast"}
+
+
 @pytest.mark.parametrize("name,batch,size", [("default", 16, 33), ("wide", 3, 33), ("tiny", 5, 15),
                                              ("default", 2, 48), ("example", 7, 33),
                                              ("default", 3, 21), ("default", 600, 33),
                                              # ragged against the grids: l3 (256 blocks, walks the
                                              # batch from its end), l12 / d1 (512 blocks)
-                                             ("default", 257, 33), ("default", 513, 33)])
+                                             ("default", 257, 33), ("default", 513, 33),
+                                             # tiles past the fused kernels' limit (33x33)
+                                             ("default", 9, 36), ("example", 5, 39)])
 def test_train_step_vs_oracle(S, path, name, batch, size):
     cfg = NETS[name]
     net = S.Net(*cfg)
@@ -323,15 +342,18 @@ def test_train_step_vs_oracle(S, path, name, batch, size):
     P = params.size
     g0 = (1e-3 * rng.standard_normal(P)).astype(np.float32)
     rg, acts = orc.train_fwd_bwd(cfg, X, T, size, size, batch, params, g0)
+    xg, _ = orc.f64.train_fwd_bwd(cfg, X, T, size, size, batch, params, g0)
     nbytes = S.train_workspace_bytes(net, size, size, batch)
     ws = torch.empty(nbytes // 4 + 64, dtype=torch.float32, device="cuda")
     g = D(g0)
     err = zeros(1)
     S.train_fwd_bwd(net, D(X), D(T), size, size, batch, D(params), g, err, ws, nbytes)
+    assert S.last_path() in expected_train_path(name, size, path), S.last_path()
     got = H(g)
     off = S.net_offsets(net) + [P]
     for i, nm in enumerate(["W1", "B1", "W2", "B2", "W3", "B3"]):
-        assert_close(got[off[i]:off[i + 1]], rg[off[i]:off[i + 1]], RTOL, "grad " + nm)
+        sl = slice(off[i], off[i + 1])
+        assert_close(got[sl], rg[sl], RTOL, "grad " + nm, xg[sl], FLIP_FLOOR)
     # validation metric over the same forward
     pad = cfg[2] + cfg[3] + cfg[4] - 3
     A3 = orc.forward(cfg, X, size, size, batch, params)
@@ -361,7 +383,7 @@ def test_forward_vs_oracle(S, path):
     ws = torch.empty(nbytes // 4 + 64, dtype=torch.float32, device="cuda")
     out = zeros(ref.size)
     S.forward(net, D(X), w, h, b, D(params), out, ws, nbytes)
-    assert_close(H(out), ref, RTOL, "forward 256x256")
+    assert_close(H(out), ref, RTOL, "forward 256x256", orc.f64.forward(cfg, X, w, h, b, params))
 
 
 FWD_FRAMES = [("default", 77, 45, 3), ("default", 300, 210, 1), ("example", 96, 64, 2),
@@ -384,12 +406,34 @@ def test_forward_frames_vs_oracle(S, path, name, w, h, b):
     S.forward(net, D(X), w, h, b, D(params), out, ws, nbytes)
     got = H(out)
     assert np.isfinite(got).all()  # every output written
-    assert_close(got, ref, RTOL, "forward %s %dx%d b%d" % (name, w, h, b))
+    assert_close(got, ref, RTOL, "forward %s %dx%d b%d" % (name, w, h, b),
+                 orc.f64.forward(cfg, X, w, h, b, params))
+
+
+def test_forward_4k_frame_vs_oracle(S):
+    """BASELINE.json configs[4] at its own size: one 3840x2160 luma frame
+    through the fused inference kernels against the oracle (OpenMP over
+    output rows), every one of the 3828x2148 outputs checked."""
+    cfg = NETS["default"]
+    net = S.Net(*cfg)
+    rng = np.random.default_rng(4096)
+    w, h = 3840, 2160
+    X, _ = make_batch(rng, 1, w, h)
+    params = make_params(rng, cfg, sd=0.05)
+    ref = orc.forward(cfg, X, w, h, 1, params)
+    nbytes = S.forward_workspace_bytes(net, w, h, 1)
+    ws = torch.empty(nbytes // 4 + 64, dtype=torch.float32, device="cuda")
+    out = torch.full((ref.size,), float("nan"), dtype=torch.float32, device="cuda")
+    S.forward(net, D(X), w, h, 1, D(params), out, ws, nbytes)
+    assert S.last_path() == "fused"
+    got = H(out)
+    assert np.isfinite(got).all()  # every output written
+    assert_close(got, ref, RTOL, "forward 3840x2160", orc.f64.forward(cfg, X, w, h, 1, params))
 
 
 def test_forward_large_frame_fused_vs_generic(S):
-    """A 1280x720 frame: the fused path against the generic layer-by-layer
-    path on the same device (the oracle would take minutes here)."""
+    """A 1280x720 frame: the fused path and the generic layer-by-layer path,
+    each against the oracle."""
     cfg = NETS["default"]
     net = S.Net(*cfg)
     rng = np.random.default_rng(720)
@@ -409,7 +453,10 @@ def test_forward_large_frame_fused_vs_generic(S):
         finally:
             S.set_path(0)
     assert np.isfinite(res[0]).all()
-    assert_close(res[0], res[1], RTOL, "forward 1280x720 fused vs generic")
+    ref = orc.forward(cfg, X, w, h, 1, params)
+    ref64 = orc.f64.forward(cfg, X, w, h, 1, params)
+    assert_close(res[0], ref, RTOL, "forward 1280x720 fused", ref64)
+    assert_close(res[1], ref, RTOL, "forward 1280x720 generic", ref64)
 
 
 # ----------------------------------------------------------------------------
@@ -424,6 +471,7 @@ def test_full_batch_gradients_vs_oracle(S):
     params = make_params(rng, cfg, sd=0.05)
     P = params.size
     rg, _ = orc.train_fwd_bwd(cfg, X, T, size, size, batch, params, np.zeros(P, np.float32))
+    xg, _ = orc.f64.train_fwd_bwd(cfg, X, T, size, size, batch, params, np.zeros(P))
     nbytes = S.train_workspace_bytes(net, size, size, batch)
     ws = torch.empty(nbytes // 4 + 64, dtype=torch.float32, device="cuda")
     Xd, Td, pd = D(X), D(T), D(params)
@@ -432,7 +480,8 @@ def test_full_batch_gradients_vs_oracle(S):
     got = H(g)
     off = S.net_offsets(net) + [P]
     for i, nm in enumerate(["W1", "B1", "W2", "B2", "W3", "B3"]):
-        assert_close(got[off[i]:off[i + 1]], rg[off[i]:off[i + 1]], RTOL, "full-batch grad " + nm)
+        sl = slice(off[i], off[i + 1])
+        assert_close(got[sl], rg[sl], RTOL, "full-batch grad " + nm, xg[sl], FLIP_FLOOR)
     # determinism: a second pass gives bit-identical gradients
     g2 = zeros(P)
     S.train_fwd_bwd(net, Xd, Td, size, size, batch, pd, g2, None, ws, nbytes)

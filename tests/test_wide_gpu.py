@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 
 import srcnn_oracle as orc
-from hip_util import RTOL, assert_close, make_batch, make_params
+from hip_util import FLIP_FLOOR, RTOL, assert_close, make_batch, make_params
 
 pytestmark = pytest.mark.gpu
 
@@ -85,6 +85,7 @@ def test_wide_step_stages_vs_oracle(S, w, h, batch):
     X, T, params, g0, got, err, ws, stats = run_step(S, w, h, batch, seed=7 + w + h + batch)
     assert "wide_l2_fwd" in stats and "wide_grad2" in stats, stats.keys()
     ref_g, acts = orc.train_fwd_bwd(WIDE, X, T, w, h, batch, params, g0, want_acts=True)
+    x_g, xacts = orc.f64.train_fwd_bwd(WIDE, X, T, w, h, batch, params, g0, want_acts=True)
     n1, n2, f1, f2, f3 = WIDE
     w1, h1 = w - f1 + 1, h - f1 + 1
     w2, h2 = w1 - f2 + 1, h1 - f2 + 1
@@ -94,13 +95,14 @@ def test_wide_step_stages_vs_oracle(S, w, h, batch):
     rA2 = acts[s1:s1 + s2]
     rD2 = acts[s1 + s2 + 2 * s3:s1 + 2 * s2 + 2 * s3]
     st = split_ws(ws, w, h, batch)
-    assert_close(st["A1"], rA1, RTOL, "A1")
-    assert_close(st["A2"], rA2, RTOL, "A2")
-    assert_close(st["D2"], rD2, RTOL, "D2")
+    assert_close(st["A1"], rA1, RTOL, "A1", xacts[:s1])
+    assert_close(st["A2"], rA2, RTOL, "A2", xacts[s1:s1 + s2])
+    assert_close(st["D2"], rD2, RTOL, "D2", xacts[s1 + s2 + 2 * s3:s1 + 2 * s2 + 2 * s3])
     net = S.Net(*WIDE)
     off = S.net_offsets(net) + [params.size]
     for i, nm in enumerate(["W1", "B1", "W2", "B2", "W3", "B3"]):
-        assert_close(got[off[i]:off[i + 1]], ref_g[off[i]:off[i + 1]], RTOL, "grad " + nm)
+        sl = slice(off[i], off[i + 1])
+        assert_close(got[sl], ref_g[sl], RTOL, "grad " + nm, x_g[sl], FLIP_FLOOR)
     A3 = orc.forward(WIDE, X, w, h, batch, params)
     ref_err = orc.sq_err(T, A3, w, h, w3, h3, batch)
     assert err == pytest.approx(ref_err, rel=1e-4)
@@ -113,7 +115,8 @@ def test_wide_step_accumulates_and_is_deterministic(S):
     g0 = (1e-3 * rng.standard_normal(orc.param_count(*WIDE))).astype(np.float32)
     X, T, params, _, got, _, _, _ = run_step(S, w, h, batch, seed=11, g0=g0)
     ref_g, _ = orc.train_fwd_bwd(WIDE, X, T, w, h, batch, params, g0)
-    assert_close(got, ref_g, RTOL, "wide gradients (accumulated onto g0)")
+    x_g, _ = orc.f64.train_fwd_bwd(WIDE, X, T, w, h, batch, params, g0)
+    assert_close(got, ref_g, RTOL, "wide gradients (accumulated onto g0)", x_g, FLIP_FLOOR)
     _, _, _, _, got2, _, _, _ = run_step(S, w, h, batch, seed=11, g0=g0)
     np.testing.assert_array_equal(got2, got)
 
@@ -130,3 +133,52 @@ def test_wide_fast_matches_generic_path(S):
     assert "wide_l2_fwd" not in gen[7]
     assert_close(fast[4], gen[4], RTOL, "fast vs generic gradients")
     assert fast[5] == pytest.approx(gen[5], rel=1e-4)
+
+
+def test_wide_full_batch_4096_vs_oracle(S):
+    """BASELINE.json configs[3] at its own size (batch 4096 of 33x33 tiles).
+    The oracle needs ~2.3 TFLOP for 4096 wide tiles (about a minute), so the
+    batch is 64 distinct tiles, each repeated 64 times: the gradient of the
+    4096-tile step is then 64 x the oracle's 64-tile gradient (the sums
+    differ only in order), and every tile's A2 / D2 equals its source tile's.
+    This runs the full-size grids, slab counts and tails of every wide kernel."""
+    w = h = 33
+    distinct, rep = 64, 64
+    batch = distinct * rep
+    net = S.Net(*WIDE)
+    rng = np.random.default_rng(4096)
+    X, T = make_batch(rng, distinct, w, h)
+    params = make_params(rng, WIDE, sd=0.05)
+    P = params.size
+    Xb, Tb = np.tile(X, rep), np.tile(T, rep)
+    nbytes = S.train_workspace_bytes(net, w, h, batch)
+    ws = torch.zeros(nbytes // 4 + 64, dtype=torch.float32, device="cuda")
+    g = torch.zeros(P, dtype=torch.float32, device="cuda")
+    S.train_fwd_bwd(net, D(Xb), D(Tb), w, h, batch, D(params), g, None, ws, nbytes)
+    assert S.last_path() == "wide"
+    got = H(g)
+    ref_g, acts = orc.train_fwd_bwd(WIDE, X, T, w, h, distinct, params, np.zeros(P, np.float32),
+                                    want_acts=True)
+    x_g, xacts = orc.f64.train_fwd_bwd(WIDE, X, T, w, h, distinct, params, np.zeros(P), want_acts=True)
+    off = S.net_offsets(net) + [P]
+    # 2.6M-term fp32 sums (64x the oracle's 64-tile sums): 2e-4 normwise, as
+    # for the other >1M-term sums (test_backpropagation_big_data), and the
+    # same as the elementwise floor (7M ReLU decisions of A1 / A2 feed these
+    # gradients, so a few fall within fp32 rounding of zero, hip_util.FLIP_FLOOR)
+    for i, nm in enumerate(["W1", "B1", "W2", "B2", "W3", "B3"]):
+        sl = slice(off[i], off[i + 1])
+        assert_close(got[sl], rep * ref_g[sl], 2e-4, "batch-4096 grad " + nm, rep * x_g[sl], 2e-4)
+    # sampled activation slices: tiles 0, 1000, 4095 (sources 0, 1000 % 64, 63)
+    n1, n2, f1, f2, f3 = WIDE
+    w1, h1 = w - f1 + 1, h - f1 + 1
+    w2, h2 = w1 - f2 + 1, h1 - f2 + 1
+    w3, h3 = w2 - f3 + 1, h2 - f3 + 1
+    s1, s2, s3 = w1 * h1 * n1, w2 * h2 * n2, w3 * h3
+    a2 = slice(s1 * distinct, (s1 + s2) * distinct)
+    d2 = slice((s1 + s2 + 2 * s3) * distinct, (s1 + 2 * s2 + 2 * s3) * distinct)
+    st = split_ws(H(ws), w, h, batch)
+    for t in (0, 1000, batch - 1):
+        src = slice((t % distinct) * s2, (t % distinct + 1) * s2)
+        mine = slice(t * s2, (t + 1) * s2)
+        assert_close(st["A2"][mine], acts[a2][src], RTOL, "A2 tile %d" % t, xacts[a2][src])
+        assert_close(st["D2"][mine], acts[d2][src], RTOL, "D2 tile %d" % t, xacts[d2][src])
