@@ -180,8 +180,10 @@ void load(const std::string& path, ImageData& img, int channels) {
     decode_png(f, img);
   else if (f.size() >= 2 && f[0] == 'P' && (f[1] == '5' || f[1] == '6'))
     decode_pnm(f, img);
+  else if (f.size() >= 3 && f[0] == 0xFF && f[1] == 0xD8 && f[2] == 0xFF)
+    decode_jpeg(f, img);
   else
-    throw IOException("unsupported image format (PNG / PNM only): " + path);
+    throw IOException("unsupported image format (JPEG / PNG / PNM only): " + path);
   convert(img, channels);
 }
 

@@ -2,25 +2,30 @@
 //
 // The reference reads/writes images with the vendored stb_image /
 // stb_image_write (src/opencl/UtilsOpenCL.cpp load_image / write_image).
-// This is an independent codec set built on the system zlib:
+// This is an independent codec set (PNG on the system zlib):
+//   JPEG read: baseline / extended / progressive Huffman, 8-bit, gray or
+//        YCbCr with any sampling factors (Jpeg.cpp) -- the reference's
+//        sample pairs and photos are JPEG (src/Main_cl.cpp:267-301)
 //   PNG  read: 8-bit gray / gray+alpha / RGB / RGBA / palette, non-interlaced;
 //        write: 8-bit gray, RGB or RGBA
 //   PNM  read/write: binary P5 (gray) / P6 (RGB)
-// JPEG is not decoded here (no decoder in the image's toolchain): convert
-// JPEG samples to PNG first (tools/make_samples.py does).
 #ifndef SRCNN_HOST_IMAGE_HPP
 #define SRCNN_HOST_IMAGE_HPP
 
 #include <string>
+#include <vector>
 
 #include "Context.hpp"
 
 namespace srcnn {
 namespace image {
 
-/** Load a PNG or PNM file (by content) into `img`; `channels` 0 keeps the
- * file's channel count, 1/3/4 converts (gray <-> RGB, alpha = 255). */
+/** Load a JPEG, PNG or PNM file (by content) into `img`; `channels` 0 keeps
+ * the file's channel count, 1/3/4 converts (gray <-> RGB, alpha = 255). */
 void load(const std::string& path, ImageData& img, int channels = 0);
+
+/** Decode a JPEG file image (Jpeg.cpp) to 1 (gray) or 3 (RGB) channels. */
+void decode_jpeg(const std::vector<unsigned char>& file, ImageData& img);
 
 /** Write `img` (bpp 1, 3 or 4) as PNG, or PNM when the path ends in
  * .pgm/.ppm/.pnm (RGBA written as RGB there). */

@@ -5,14 +5,13 @@
 //       [--seed N] [--device D] [--devices N] [--validation-percent P]
 //       [--mini-batches M]
 //
-// forward:  IN is an image (PNG / PNM), OUT the upscaled result image
+// forward:  IN is an image (JPEG / PNG / PNM), OUT the upscaled result image
 // train:    IN is a directory of <name>_large.<ext> / <name>_small.<ext> pairs
 //           (ground truth / degraded input, tools/make_samples.py makes
 //           them), OUT the parameters.json written at the end.
 // Differences from the reference, on purpose: paths are joined with '/'
 // (the reference hard-codes "\\", src/Main_cl.cpp:284-287), the epoch
-// shuffle is seeded (--seed; the reference uses unseeded rand()), JPEG is
-// not decoded (see host/src/Image.hpp).
+// shuffle is seeded (--seed; the reference uses unseeded rand()).
 // Extension: `train --devices N` trains data-parallel on devices D .. D+N-1
 // of one node: one host thread per device, the epoch's training set sharded
 // contiguously over them, one RCCL all-reduce of the flat gradient buffer per

@@ -142,3 +142,28 @@ def test_cli_profile_output_parses_with_reference_regex(tmp_path):
         assert int(ns) >= 0 and abs(float(s) - int(ns) / 1e9) <= 1e-6 + 1e-3 * float(s)
     train = [x for x in found if x[0].startswith("srcnn_train_fwd_bwd")][0]
     assert int(train[1]) > 0  # device time was recorded
+
+
+@pytest.mark.gpu
+def test_cli_trains_on_reference_jpeg_samples(tmp_path):
+    """The reference's sample layout: <name>_large.jpg / <name>_small.jpg
+    pairs (generate_training_samples.py:36-41, src/Main_cl.cpp:267-301),
+    decoded by host/src/Jpeg.cpp; then a JPEG photo through forward."""
+    samples = tmp_path / "samples"
+    subprocess.check_call([sys.executable, MAKE_SAMPLES, "--synthetic", "4", "--per-image", "4",
+                           "-o", str(samples), "-s", "33", "--seed", "6", "--format", "jpg"])
+    assert any(f.endswith("_large.jpg") for f in os.listdir(samples))
+    params = tmp_path / "p.json"
+    p = cnn(*_train_args(tmp_path, samples, params))
+    print(p.stdout[-2000:])
+    assert p.returncode == 0 and "DONE" in p.stdout, p.stdout
+    assert "Skipping sample" not in p.stdout
+    cfg2 = tmp_path / "config2.json"
+    write_config(cfg2, str(params))
+    from PIL import Image
+    src = tmp_path / "photo.jpg"
+    Image.open(samples / "sample_0_small.jpg").resize((72, 56)).save(src, quality=90, subsampling=2)
+    out = tmp_path / "out.png"
+    p = cnn("-c", str(cfg2), "-i", str(src), "-o", str(out))
+    assert p.returncode == 0, p.stdout
+    assert Image.open(out).size == (72, 56)

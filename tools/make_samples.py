@@ -3,8 +3,9 @@
 generate_training_samples.py, re-done): from every image of --in-dir, crop a
 random --out-size square (the ground truth, <name>_large.png) and degrade it
 by downscaling with --degrade-factor and upscaling back with Lanczos
-resampling (the network input, <name>_small.png).  PNG instead of the
-reference's JPEG: lossless, and what the C++ side decodes.
+resampling (the network input, <name>_small.png).  PNG by default
+(lossless); --format jpg writes the reference's JPEG pairs, which the C++
+side decodes too (host/src/Jpeg.cpp).
 
   python tools/make_samples.py -i raw_dir -o samples_dir -s 33 -d 2 [--per-image N] [--seed S]
   python tools/make_samples.py --synthetic 64 -o samples_dir -s 33      # no input images needed
@@ -44,6 +45,9 @@ def main():
     ap.add_argument("--per-image", type=int, default=1, help="crops per input image")
     ap.add_argument("--synthetic", type=int, default=0, help="generate N synthetic source images")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--format", choices=["png", "jpg"], default="png",
+                    help="jpg writes <name>_large.jpg / _small.jpg like the reference's "
+                         "generate_training_samples.py:36-41 (PIL default quality)")
     a = ap.parse_args()
     rnd = random.Random(a.seed)
     rng = np.random.default_rng(a.seed)
@@ -72,8 +76,8 @@ def main():
             y = rnd.randint(0, im.height - a.out_size)
             large = im.crop((x, y, x + a.out_size, y + a.out_size))
             base = os.path.join(a.out_dir, "sample_%d" % n)
-            large.save(base + "_large.png")
-            degrade(large, a.degrade_factor).save(base + "_small.png")
+            large.save(base + "_large." + a.format)
+            degrade(large, a.degrade_factor).save(base + "_small." + a.format)
             n += 1
     print("created %d sample pairs" % n if n else "No files were created")
 
