@@ -51,13 +51,15 @@ int train_fwd_bwd(const srcnn_net* net, const float* X, const float* T, uint32_t
 int forward(const srcnn_net* net, const float* X, uint32_t w, uint32_t h, uint32_t batch,
             const float* params, float* out, void* ws, size_t ws_bytes, hipStream_t s,
             bool query_only, size_t* need);
-// Deterministic slab reduction shared by the fused families: for every
-// segment, dst[i] += sum_{b < nslab} slab[b * P + i], summed in block order.
+// Deterministic slab reduction shared by the fused families and the op-level
+// gradient kernels: for every segment, dst[i] += sum_{b < nslab}
+// slab[b * stride + i] (i < P), summed in block order.
 constexpr int kMaxSlabSegs = 4;
 struct SlabSeg {
   const float* slab;
   float* dst;
   int nslab, P;
+  int stride;  // floats between consecutive slabs (0 = P)
 };
 int reduce_slabs(const SlabSeg* segs, int nseg, hipStream_t s);
 // held-clock probes (common.hpp): slot 0 l12_fwd, 1 l3_delta, 2 d1_grad12
@@ -74,6 +76,19 @@ int train_fwd_bwd(const srcnn_net* net, const float* X, const float* T, uint32_t
                   uint32_t batch, const float* params, float* grads, float* sq_err, float* A1,
                   float* D1, float* A2, float* D2, float* slab, size_t slab_bytes, hipStream_t s,
                   bool query_only, size_t* need);
+// op-level launchers of the 5x5 128 <-> 64 middle layer (same contract as
+// the fast::try_* functions: 1 handled, 0 not this shape, < 0 error)
+int op_conv_fwd(const float* in, float* out, const float* W, const float* B, uint32_t in_w,
+                uint32_t in_h, uint32_t n_prev, uint32_t n_cur, uint32_t f, int relu,
+                uint32_t batch, hipStream_t s);
+int op_conv_delta(const float* d_next, const float* y_curr, float* d_curr, const float* W_next,
+                  uint32_t f_next, uint32_t n_curr, uint32_t n_next, uint32_t curr_w,
+                  uint32_t curr_h, uint32_t batch, hipStream_t s);
+size_t op_grad_workspace_bytes(uint32_t n_prev, uint32_t n_cur, uint32_t f, uint32_t out_w,
+                               uint32_t out_h, uint32_t batch);
+int op_conv_grad_acc(const float* in, const float* d, float* gW, float* gB, uint32_t n_prev,
+                     uint32_t n_cur, uint32_t f, uint32_t out_w, uint32_t out_h, uint32_t batch,
+                     void* ws, size_t ws_bytes, hipStream_t s);
 }  // namespace wide
 
 int sgd_update(float* W, float* B, const float* gW, const float* gB, float* dW, float* dB,

@@ -4,6 +4,7 @@
 // (Context.cpp:70-72); allocations are raw device pointers instead of
 // index-addressed MemoryHandles (the C++ cnn_sr::Context keeps the handles).
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -16,7 +17,13 @@
 namespace srcnn {
 
 static thread_local std::string t_last_error;
-int g_path = 0;
+// SRCNN_PATH=generic in the environment starts the library on the generic
+// kernels (A/B runs of programs that do not call srcnn_set_path themselves)
+static int initial_path() {
+  const char* e = getenv("SRCNN_PATH");
+  return e && !strcmp(e, "generic") ? 1 : 0;
+}
+int g_path = initial_path();
 
 int fail(int code, const char* fmt, ...) {
   char buf[1024];

@@ -789,9 +789,10 @@ __global__ __launch_bounds__(1024) void slab_reduce_kernel(SlabSegs ss) {
   const SlabSeg sg = ss.seg[k];
   const int cl = threadIdx.x % kSlabCols, row = threadIdx.x / kSlabCols;
   const int col = ((int)blockIdx.x - ss.first[k]) * kSlabCols + cl;
+  const size_t stride = sg.stride ? sg.stride : sg.P;
   float acc = 0.0f;
   if (col < sg.P)
-    for (int b = row; b < sg.nslab; b += kSlabRows) acc += sg.slab[(size_t)b * sg.P + col];
+    for (int b = row; b < sg.nslab; b += kSlabRows) acc += sg.slab[(size_t)b * stride + col];
   part[row][cl] = acc;
   __syncthreads();
   if (row == 0 && col < sg.P) {
@@ -811,7 +812,7 @@ int reduce_slabs(const SlabSeg* segs, int nseg, hipStream_t s) {
       ss.seg[k] = segs[k];
       blocks += (segs[k].P + kSlabCols - 1) / kSlabCols;
     } else {
-      ss.seg[k] = SlabSeg{nullptr, nullptr, 0, 0};
+      ss.seg[k] = SlabSeg{nullptr, nullptr, 0, 0, 0};
     }
   }
   ss.first[kMaxSlabSegs] = blocks;
@@ -902,9 +903,9 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   }
   {
     SRCNN_PROFILE("slab_reduce", s);
-    const SlabSeg segs[3] = {{slab12, grads, gd, NetT::P12},
-                             {slab3, grads + NetT::P12, g3, NetT::P3},
-                             {sqs, sq_err, g3, 1}};
+    const SlabSeg segs[3] = {{slab12, grads, gd, NetT::P12, 0},
+                             {slab3, grads + NetT::P12, g3, NetT::P3, 0},
+                             {sqs, sq_err, g3, 1, 0}};
     int rc = reduce_slabs(segs, sq_err ? 3 : 2, s);
     if (rc) return rc;
   }

@@ -23,6 +23,10 @@
 //   slab_reduce  fixed-order sum of the slabs into the gradient buffer
 //
 // Deterministic: static work assignment, fixed summation order, no atomics.
+#include <map>
+#include <mutex>
+#include <utility>
+
 #include "common.hpp"
 #include "mfma.hpp"
 #include "ops.hpp"
@@ -886,6 +890,137 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
                                     {slab3, grads + NetT::P1 + NetT::P2, G3, NetT::P3},
                                     {sqs, sq_err, G3, 1}};
     if (int rc = fused::reduce_slabs(segs, sq_err ? 4 : 3, s)) return rc;
+  }
+  return 1;
+}
+
+// ---------------------------------------------------------------------------
+// op-level entry points (srcnn_conv_fwd / _delta / _grad_acc through
+// ops_fast.hip) for the wide middle layer: 5x5, n1 = 128 <-> n2 = 64, the
+// same kernels as the net-level step, over the caller's reference-layout
+// buffers.  The operand images of W2 live in a per-(device, stream) buffer
+// of the library.  1 = handled,
+// 0 = shape not served here, < 0 = error.
+// ---------------------------------------------------------------------------
+namespace {
+using WideNet = Net<128, 64, 9, 5, 5>;
+constexpr int kWN1 = 128, kWN2 = 64, kWF = 5;
+
+// W2 operand images of the op-level calls: one device buffer per (device,
+// stream), kept for the process (2 x 819 KB).  Calls on one stream are
+// ordered, so a stream's buffer is never in use by two calls at once.
+std::mutex g_img_mu;
+std::map<std::pair<int, hipStream_t>, float*> g_img;
+
+int prepacked_w2(const float* W2, float** img, hipStream_t s) {
+  int dev = 0;
+  SRCNN_HIP_TRY(hipGetDevice(&dev));
+  {
+    std::lock_guard<std::mutex> lk(g_img_mu);
+    float*& buf = g_img[{dev, s}];
+    if (!buf) SRCNN_HIP_TRY(hipMalloc(reinterpret_cast<void**>(&buf), 2 * align_f(WideNet::W2) * sizeof(float)));
+    *img = buf;
+  }
+  SRCNN_PROFILE("wide_prepack_w2", s);
+  const int tot = 2 * WideNet::W2;
+  hipLaunchKernelGGL((prepack_w2_kernel<kWN1, kWN2, kWF>), dim3((tot + 255) / 256), dim3(256), 0, s, W2,
+                     *img, *img + align_f(WideNet::W2));
+  SRCNN_LAUNCH_TRY();
+  return SRCNN_OK;
+}
+}  // namespace
+
+int op_conv_fwd(const float* in, float* out, const float* W, const float* B, uint32_t in_w,
+                uint32_t in_h, uint32_t n_prev, uint32_t n_cur, uint32_t f, int relu,
+                uint32_t batch, hipStream_t s) {
+  if (n_prev != kWN1 || n_cur != kWN2 || f != kWF || !relu) return 0;
+  const int ow = (int)in_w - kWF + 1, oh = (int)in_h - kWF + 1;
+  CGeom cf{(int)in_w, (int)in_h, 0, (int)in_w, (int)in_h, ow, oh, ow * oh, (int)batch, 0, 0};
+  if ((cf.npx + 31) / 32 > 2 * WideNet::MT2 || cf.img_w * cf.img_h > kImgMax) return 0;
+  float* img = nullptr;
+  if (int rc = prepacked_w2(W, &img, s)) return rc;
+  const size_t lds = 2 * ((size_t)cf.img_w * cf.img_h * kPS + kImgSlack) * sizeof(float);
+  if (int rc = set_lds(conv_mfma_kernel<kWN1, kWN2, kWF, WideNet::MT2, false, 0>, lds)) return rc;
+  {
+    SRCNN_PROFILE("conv_fwd_wide_mfma", s);
+    const int items = (int)batch * (kWN2 / 64);
+    hipLaunchKernelGGL((conv_mfma_kernel<kWN1, kWN2, kWF, WideNet::MT2, false, 0>),
+                       dim3(std::min(items, 256)), dim3(256), lds, s, in, img, B,
+                       (const float*)nullptr, out, (const float*)nullptr, (float*)nullptr, cf);
+    SRCNN_LAUNCH_TRY();
+  }
+  return 1;
+}
+
+int op_conv_delta(const float* d_next, const float* y_curr, float* d_curr, const float* W_next,
+                  uint32_t f_next, uint32_t n_curr, uint32_t n_next, uint32_t curr_w,
+                  uint32_t curr_h, uint32_t batch, hipStream_t s) {
+  if (n_curr != kWN1 || n_next != kWN2 || f_next != kWF) return 0;
+  const int nw = (int)curr_w - kWF + 1, nh = (int)curr_h - kWF + 1;
+  CGeom cd{nw, nh, kWF - 1, nw + 2 * (kWF - 1), nh + 2 * (kWF - 1), (int)curr_w, (int)curr_h,
+           (int)(curr_w * curr_h), (int)batch, 0, 0};
+  if ((cd.npx + 31) / 32 > 2 * WideNet::MT4 || cd.img_w * cd.img_h > kImgMax) return 0;
+  float* img = nullptr;
+  if (int rc = prepacked_w2(W_next, &img, s)) return rc;
+  const size_t lds = 2 * ((size_t)cd.img_w * cd.img_h * kPS + kImgSlack) * sizeof(float);
+  if (int rc = set_lds(conv_mfma_kernel<kWN2, kWN1, kWF, WideNet::MT4, true, 0>, lds)) return rc;
+  {
+    SRCNN_PROFILE("conv_delta_wide_mfma", s);
+    const int items = (int)batch * (kWN1 / 64);
+    hipLaunchKernelGGL((conv_mfma_kernel<kWN2, kWN1, kWF, WideNet::MT4, true, 0>),
+                       dim3(std::min(items, 256)), dim3(256), lds, s, d_next,
+                       img + align_f(WideNet::W2), (const float*)nullptr, y_curr, d_curr,
+                       (const float*)nullptr, (float*)nullptr, cd);
+    SRCNN_LAUNCH_TRY();
+  }
+  return 1;
+}
+
+namespace {
+bool g2_geom(uint32_t out_w, uint32_t out_h, uint32_t batch, G2Geom* g2) {
+  g2->w2 = (int)out_w;
+  g2->h2 = (int)out_h;
+  g2->w1 = g2->w2 + kWF - 1;
+  g2->h1 = g2->h2 + kWF - 1;
+  g2->rows = std::min(8, kBandPx / std::max(1, g2->w2));
+  if (g2->rows < 1 || (g2->rows + kWF - 1) * g2->w1 > kGAPx) return false;
+  g2->nbands = (g2->h2 + g2->rows - 1) / g2->rows;
+  g2->batch = (int)batch;
+  g2->groups = (int)std::min<uint32_t>(batch, 64);
+  return true;
+}
+}  // namespace
+
+size_t op_grad_workspace_bytes(uint32_t n_prev, uint32_t n_cur, uint32_t f, uint32_t out_w,
+                               uint32_t out_h, uint32_t batch) {
+  G2Geom g2;
+  if (n_prev != kWN1 || n_cur != kWN2 || f != kWF || !g2_geom(out_w, out_h, batch, &g2)) return 0;
+  return (size_t)g2.groups * WideNet::P2 * sizeof(float);
+}
+
+int op_conv_grad_acc(const float* in, const float* d, float* gW, float* gB, uint32_t n_prev,
+                     uint32_t n_cur, uint32_t f, uint32_t out_w, uint32_t out_h, uint32_t batch,
+                     void* ws, size_t ws_bytes, hipStream_t s) {
+  G2Geom g2;
+  if (n_prev != kWN1 || n_cur != kWN2 || f != kWF || !g2_geom(out_w, out_h, batch, &g2)) return 0;
+  const size_t need = (size_t)g2.groups * WideNet::P2 * sizeof(float);
+  if (ws_bytes < need)
+    return fail(SRCNN_ERR_WORKSPACE, "backpropagate: workspace %zu B < %zu B", ws_bytes, need);
+  float* slab2 = static_cast<float*>(ws);
+  {
+    SRCNN_PROFILE("grad_wide_mfma", s);
+    const size_t lds = 2 * (size_t)kGBuf * sizeof(float);
+    if (int rc = set_lds(wgrad2_kernel<kWN1, kWN2, kWF>, lds)) return rc;
+    hipLaunchKernelGGL((wgrad2_kernel<kWN1, kWN2, kWF>), dim3(g2.groups * (kWN1 / 32)), dim3(512), lds,
+                       s, in, d, slab2, g2);
+    SRCNN_LAUNCH_TRY();
+  }
+  {
+    SRCNN_PROFILE("slab_reduce", s);
+    const int nW = WideNet::W2;
+    const fused::SlabSeg segs[2] = {{slab2, gW, g2.groups, nW, WideNet::P2},
+                                    {slab2 + nW, gB, g2.groups, kWN2, WideNet::P2}};
+    if (int rc = fused::reduce_slabs(segs, 2, s)) return rc;
   }
   return 1;
 }

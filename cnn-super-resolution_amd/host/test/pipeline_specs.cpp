@@ -465,6 +465,10 @@ void cbdp_spec(DataPipeline* p, size_t n1, size_t n2, size_t f1, size_t f2, size
     }
     float err = pipe.execute_batch(false, pools, set);
     expect(std::isfinite(err) && err > 0.f, "validation error");
+    if (getenv("SRCNN_SPEC_DEBUG")) {
+      float err2 = pipe.execute_batch(false, pools, set);
+      std::cout << "variant " << variant << " validation error " << err << " / again " << err2 << std::endl;
+    }
     std::string path = "/tmp/srcnn_cbdp_params_" + std::to_string(variant) + ".json";
     pipe.write_params_to_file(path.c_str(), pools.layer_1, pools.layer_2, pools.layer_3);
     std::vector<float>& r = results[variant];
@@ -489,7 +493,12 @@ void cbdp_spec(DataPipeline* p, size_t n1, size_t n2, size_t f1, size_t f2, size
     expect(std::fabs(results[0][i] - results[1][i]) <= 1e-4 * (std::fabs(results[0][i]) + scale),
            "fused and op-level training disagree at " + std::to_string(i));
   float e0 = results[0].back(), e1 = results[1].back();
-  expect(std::fabs(e0 - e1) <= 1e-3f * std::fabs(e1), "validation error mismatch");
+  double dmax = 0;
+  for (size_t i = 0; i + 1 < results[0].size(); ++i)
+    dmax = std::max(dmax, std::fabs(double(results[0][i]) - results[1][i]) / scale);
+  expect(std::fabs(e0 - e1) <= 1e-3f * std::fabs(e1),
+         "validation error mismatch: fused " + std::to_string(e0) + ", op path " + std::to_string(e1) +
+             " (max parameter difference " + std::to_string(dmax) + " of the largest)");
 }
 
 // forward(sample) + write_result_image on a synthetic RGBA image

@@ -4,8 +4,9 @@ and the reference's golden vectors.
 Tolerance: fp32, normwise 1e-4 (hip_util.RTOL) unless a fixture's own
 printed precision is coarser (then that precision, as in
 test_oracle_golden.py).  Integer / byte outputs (swap_luma) are exact.
-Every parametrised case runs on both kernel paths: "auto" (gfx950
-specialisations where the shape matches) and "generic".
+Every parametrised op-level case runs on both kernel paths: "auto" (the
+ops_fast.hip gfx950 kernels where the shape matches, asserted through
+srcnn_last_path) and "generic".
 """
 import json
 import os
@@ -224,22 +225,38 @@ def test_swap_luma_spec(S):
 # random shapes vs the oracle (including the SRCNN default / wide layers)
 # ----------------------------------------------------------------------------
 FWD_SHAPES = [
-    # (n_prev, n_cur, f, in_w, in_h, batch, relu)
-    (1, 64, 9, 33, 33, 5, 1),     # default L1
-    (64, 32, 1, 25, 25, 5, 1),    # default L2
-    (32, 1, 5, 25, 25, 5, 0),     # default L3 (SKIP_RELU)
-    (1, 128, 9, 33, 33, 2, 1),    # wide L1
-    (128, 64, 5, 25, 25, 2, 1),   # wide L2
-    (64, 1, 5, 21, 21, 2, 0),     # wide L3
-    (3, 7, 3, 11, 9, 3, 1),       # ragged
-    (1, 1, 1, 1, 1, 1, 0),        # minimal
-    (1, 64, 9, 40, 37, 3, 1),     # non-square, not a 33 tile
+    # (n_prev, n_cur, f, in_w, in_h, batch, relu, served by ops_fast.hip on the auto path)
+    (1, 64, 9, 33, 33, 5, 1, True),     # default L1
+    (64, 32, 1, 25, 25, 5, 1, True),    # default L2
+    (32, 1, 5, 25, 25, 5, 0, True),     # default L3 (SKIP_RELU)
+    (1, 128, 9, 33, 33, 2, 1, True),    # wide L1
+    (128, 64, 5, 25, 25, 2, 1, True),   # wide L2
+    (64, 1, 5, 21, 21, 2, 0, True),     # wide L3
+    (3, 7, 3, 11, 9, 3, 1, False),      # ragged
+    (1, 1, 1, 1, 1, 1, 0, False),       # minimal
+    (1, 64, 9, 40, 37, 3, 1, True),     # non-square, not a 33 tile
+    (1, 32, 9, 33, 33, 3, 1, True),     # example L1
+    (32, 16, 1, 25, 25, 3, 1, True),    # example L2
+    (16, 1, 5, 25, 25, 3, 0, True),     # example L3
+    (64, 32, 1, 7, 5, 1, 0, True),      # pointwise: ragged pixel count, no ReLU
+    (1, 64, 9, 41, 41, 2, 1, False),    # tile past the layer-1 kernel's LDS image
+    (128, 64, 5, 25, 25, 1, 0, False),  # wide L2 without ReLU: generic
+    # the wide net on 25x25 tiles (host spec geometry)
+    (1, 128, 9, 25, 25, 3, 1, True),
+    (128, 64, 5, 17, 17, 3, 1, True),
+    (64, 1, 5, 13, 13, 3, 0, True),
 ]
+
+
+def check_path(S, path, fast):
+    """The op-level call ran the gfx950 kernel it was meant to (auto path)."""
+    want = "fast" if (path == 0 and fast) else "generic"
+    assert S.last_path() == want, (S.last_path(), want)
 
 
 @pytest.mark.parametrize("shape", FWD_SHAPES, ids=lambda s: "k%d_n%d_f%d_%dx%d_b%d" % s[:6])
 def test_conv_fwd_vs_oracle(S, path, shape):
-    n_prev, n_cur, f, iw, ih, b, relu = shape
+    n_prev, n_cur, f, iw, ih, b, relu, fast = shape
     rng = np.random.default_rng(hash(shape) & 0xFFFF)
     x = rng.standard_normal(b * iw * ih * n_prev).astype(np.float32)
     W = (rng.standard_normal(f * f * n_prev * n_cur) / np.sqrt(f * f * n_prev)).astype(np.float32)
@@ -247,23 +264,29 @@ def test_conv_fwd_vs_oracle(S, path, shape):
     ref = orc.conv_fwd(x, W, B, iw, ih, n_prev, n_cur, f, relu, b)
     out = zeros(ref.size)
     S.conv_fwd(D(x), out, D(W), D(B), iw, ih, n_prev, n_cur, f, relu, b)
+    check_path(S, path, fast)
     assert_close(H(out), ref, RTOL, "conv_fwd", orc.f64.conv_fwd(x, W, B, iw, ih, n_prev, n_cur, f, relu, b))
 
 
 DELTA_SHAPES = [
-    # (n_curr, n_next, f_next, curr_w, curr_h, batch)
-    (32, 1, 5, 25, 25, 4),    # default delta2 (through W3)
-    (64, 32, 1, 25, 25, 4),   # default delta1 (through W2)
-    (64, 1, 5, 21, 21, 2),    # wide delta2
-    (128, 64, 5, 25, 25, 2),  # wide delta1
-    (2, 3, 3, 5, 5, 1),       # LayerDeltasTest shape
-    (5, 4, 3, 9, 7, 3),       # ragged
+    # (n_curr, n_next, f_next, curr_w, curr_h, batch, served by ops_fast.hip on auto)
+    (32, 1, 5, 25, 25, 4, True),     # default delta2 (through W3)
+    (64, 32, 1, 25, 25, 4, True),    # default delta1 (through W2)
+    (64, 1, 5, 21, 21, 2, True),     # wide delta2
+    (128, 64, 5, 25, 25, 2, True),   # wide delta1
+    (2, 3, 3, 5, 5, 1, False),       # LayerDeltasTest shape
+    (5, 4, 3, 9, 7, 3, False),       # ragged
+    (16, 1, 5, 25, 25, 3, True),     # example delta2
+    (32, 16, 1, 25, 25, 3, True),    # example delta1
+    (32, 1, 3, 9, 6, 2, True),       # f3 = 3, non-square
+    (64, 1, 5, 13, 13, 3, True),     # wide net, 25x25 tiles
+    (128, 64, 5, 17, 17, 3, True),
 ]
 
 
-@pytest.mark.parametrize("shape", DELTA_SHAPES, ids=lambda s: "n%d_k%d_f%d_%dx%d_b%d" % s)
+@pytest.mark.parametrize("shape", DELTA_SHAPES, ids=lambda s: "n%d_k%d_f%d_%dx%d_b%d" % s[:6])
 def test_conv_delta_vs_oracle(S, path, shape):
-    n_curr, n_next, f, cw, ch, b = shape
+    n_curr, n_next, f, cw, ch, b, fast = shape
     rng = np.random.default_rng(hash(shape) & 0xFFFF)
     nw, nh = cw - f + 1, ch - f + 1
     d_next = rng.standard_normal(b * nw * nh * n_next).astype(np.float32)
@@ -272,23 +295,33 @@ def test_conv_delta_vs_oracle(S, path, shape):
     ref = orc.conv_delta(d_next, y, W, f, n_curr, n_next, cw, ch, b)
     out = zeros(ref.size)
     S.conv_delta(D(d_next), D(y), out, D(W), f, n_curr, n_next, cw, ch, b)
+    check_path(S, path, fast)
     assert_close(H(out), ref, RTOL, "conv_delta",
                  orc.f64.conv_delta(d_next, y, W, f, n_curr, n_next, cw, ch, b))
 
 
 GRAD_SHAPES = [
-    # (n_prev, n_cur, f, out_w, out_h, batch)
-    (1, 64, 9, 25, 25, 6),    # default gW1
-    (64, 32, 1, 25, 25, 6),   # default gW2
-    (32, 1, 5, 21, 21, 6),    # default gW3
-    (128, 64, 5, 21, 21, 2),  # wide gW2
-    (3, 5, 3, 7, 6, 3),       # ragged
+    # (n_prev, n_cur, f, out_w, out_h, batch, served by ops_fast.hip on auto)
+    (1, 64, 9, 25, 25, 6, True),     # default gW1
+    (64, 32, 1, 25, 25, 6, True),    # default gW2
+    (32, 1, 5, 21, 21, 6, True),     # default gW3
+    (128, 64, 5, 21, 21, 2, True),   # wide gW2
+    (3, 5, 3, 7, 6, 3, False),       # ragged
+    (1, 128, 9, 25, 25, 3, True),    # wide gW1
+    (64, 1, 5, 17, 17, 3, True),     # wide gW3
+    (1, 32, 9, 25, 25, 3, True),     # example gW1
+    (32, 16, 1, 25, 25, 3, True),    # example gW2
+    (16, 1, 5, 21, 21, 3, True),     # example gW3
+    (64, 32, 1, 5, 3, 1, True),      # pointwise, 15 pixels
+    (64, 1, 5, 9, 9, 3, True),       # wide net, 25x25 tiles
+    (128, 64, 5, 13, 13, 3, True),
+    (1, 128, 9, 17, 17, 3, True),
 ]
 
 
-@pytest.mark.parametrize("shape", GRAD_SHAPES, ids=lambda s: "k%d_n%d_f%d_%dx%d_b%d" % s)
+@pytest.mark.parametrize("shape", GRAD_SHAPES, ids=lambda s: "k%d_n%d_f%d_%dx%d_b%d" % s[:6])
 def test_conv_grad_vs_oracle(S, path, shape):
-    n_prev, n_cur, f, ow, oh, b = shape
+    n_prev, n_cur, f, ow, oh, b, fast = shape
     rng = np.random.default_rng(hash(shape) & 0xFFFF)
     iw, ih = ow + f - 1, oh + f - 1
     inp = rng.standard_normal(b * iw * ih * n_prev).astype(np.float32)
@@ -300,6 +333,7 @@ def test_conv_grad_vs_oracle(S, path, shape):
     ws = zeros(nbytes // 4 + 1)
     gW, gB = D(gW0), D(gB0)
     S.conv_grad_acc(D(inp), D(dl), gW, gB, n_prev, n_cur, f, ow, oh, b, ws, nbytes)
+    check_path(S, path, fast)
     xW, xB = orc.f64.conv_grad_acc(inp, dl, gW0, gB0, n_prev, n_cur, f, ow, oh, b)
     assert_close(H(gW), rW, RTOL, "gW", xW)
     assert_close(H(gB), rB, RTOL, "gB", xB)
