@@ -320,7 +320,10 @@ constexpr int kD1Diag = SRCNN_D1_DIAG;
 constexpr int kD1Diag = 0;
 #endif
 constexpr bool kD1DiagNoD1 = kD1Diag & 1, kD1DiagNoGW2 = kD1Diag & 2, kD1DiagNoMask = kD1Diag & 4,
-               kD1DiagNoGW1 = kD1Diag & 8, kD1DiagNoDma = kD1Diag & 16;
+               kD1DiagNoGW1 = kD1Diag & 8, kD1DiagNoDma = kD1Diag & 16,
+               // 32: gW1 X gathers at lane-linear (bank-conflict-free) addresses;
+               // 64: delta1 operand reads at lane-linear addresses
+               kD1DiagLinX = kD1Diag & 32, kD1DiagLinD1 = kD1Diag & 64;
 #ifndef SRCNN_D1_D2SW
 #define SRCNN_D1_D2SW 1
 #endif
@@ -545,9 +548,10 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
         float a[2], b[NQ];
 #pragma unroll
         for (int pm = 0; pm < 2; pm++)
-          a[pm] = d2me[kD1D2Sw ? (dab ^ (4 * s)) + 16 * pm * DS : (16 * pm + lq) * DS + n];
+          a[pm] = kD1DiagLinD1 ? d2me[lane + 64 * ((s + pm) & 7)]
+                               : d2me[kD1D2Sw ? (dab ^ (4 * s)) + 16 * pm * DS : (16 * pm + lq) * DS + n];
 #pragma unroll
-        for (int t = 0; t < NQ; t++) b[t] = w2s[(16 * t + lq) * WS + n];
+        for (int t = 0; t < NQ; t++) b[t] = kD1DiagLinD1 ? w2s[lane + 64 * ((s + t) & 7)] : w2s[(16 * t + lq) * WS + n];
 #pragma unroll
         for (int pm = 0; pm < 2; pm++)
 #pragma unroll
@@ -634,7 +638,7 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
         {
           const int xb = SRCNN_D1_XB(0);
 #pragma unroll
-          for (int m = 0; m < MT; m++) acur[m] = xs[xb + toff[m]];
+          for (int m = 0; m < MT; m++) acur[m] = kD1DiagLinX ? xs[(lane + 64 * m + xb) & 1023] : xs[xb + toff[m]];
 #pragma unroll
           for (int r = 0; r < KR; r++) {
             const int tap = 16 * MT + r;
@@ -648,7 +652,7 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
           if (s + 1 < 8) {
             const int xb = SRCNN_D1_XB(s + 1);
 #pragma unroll
-            for (int m = 0; m < MT; m++) anxt[m] = xs[xb + toff[m]];
+            for (int m = 0; m < MT; m++) anxt[m] = kD1DiagLinX ? xs[(lane + 64 * m + xb) & 1023] : xs[xb + toff[m]];
 #pragma unroll
             for (int r = 0; r < KR; r++) {
               const int tap = 16 * MT + r;
