@@ -263,8 +263,8 @@ size_t srcnn_train_workspace_bytes(const srcnn_net* net, uint32_t w, uint32_t h,
   size_t fused_need = 0;
   if (fast_enabled() &&
       srcnn::fused::train_fwd_bwd(net, nullptr, nullptr, w, h, batch, nullptr, nullptr, nullptr,
-                                  nullptr, nullptr, nullptr, nullptr, 0, nullptr, true,
-                                  &fused_need) == 1)
+                                  nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr,
+                                  true, &fused_need) == 1)
     g = std::max(g, fused_need);
   size_t wide_need = 0;
   if (fast_enabled() &&
@@ -308,9 +308,9 @@ int srcnn_train_fwd_bwd(const srcnn_net* net, const float* X, const float* T, ui
         *gB2 = grads + off[3], *gW3 = grads + off[4], *gB3 = grads + off[5];
   int rc;
   if (fast_enabled()) {
-    rc = srcnn::fused::train_fwd_bwd(net, X, T, w, h, batch, params, grads, sq_err, A1, A2, D2,
-                                     static_cast<float*>(gws), gws_bytes, srcnn::as_stream(stream),
-                                     false, nullptr);
+    rc = srcnn::fused::train_fwd_bwd(net, X, T, w, h, batch, params, grads, sq_err, A1, A2, D2, A3,
+                                     D3, static_cast<float*>(gws), gws_bytes,
+                                     srcnn::as_stream(stream), false, nullptr);
     if (rc != 0) return rc < 0 ? rc : tag("fused", SRCNN_OK);
     rc = srcnn::wide::train_fwd_bwd(net, X, T, w, h, batch, params, grads, sq_err, A1, D1, A2, D2,
                                     static_cast<float*>(gws), gws_bytes, srcnn::as_stream(stream),

@@ -44,8 +44,8 @@ int try_conv_grad_acc(const float* in, const float* d, float* gW, float* gB, uin
 namespace fused {
 int train_fwd_bwd(const srcnn_net* net, const float* X, const float* T, uint32_t w, uint32_t h,
                   uint32_t batch, const float* params, float* grads, float* sq_err, float* A1,
-                  float* A2, float* D2, float* slab, size_t slab_bytes, hipStream_t s,
-                  bool query_only, size_t* need);
+                  float* A2, float* D2, float* A3, float* D3, float* slab, size_t slab_bytes,
+                  hipStream_t s, bool query_only, size_t* need);
 // Fused inference (forward_fused.hip): 1 when specialised (with query_only:
 // workspace bytes in *need), 0 when not.
 int forward(const srcnn_net* net, const float* X, uint32_t w, uint32_t h, uint32_t batch,

@@ -672,7 +672,8 @@ size_t l3_fwd_lds(int F3, uint32_t w2, uint32_t h2) { return (size_t)w2 * h2 * F
 size_t d3_lds(int F3, uint32_t w2, uint32_t h2) {
   return ((size_t)w2 * h2 + (F3 - 1) * (w2 + 1) + 4) * sizeof(float);
 }
-constexpr size_t kLdsCap = 64 * 1024;
+constexpr size_t kLdsCap = 64 * 1024;   // the default dynamic LDS of a launch
+constexpr size_t kLdsMax = 160 * 1024;  // with hipFuncSetAttribute (one block per CU)
 
 }  // namespace
 
@@ -709,11 +710,12 @@ int try_conv_fwd(const float* in, float* out, const float* W, const float* B, ui
 #undef SRCNN_L1_F
     return 0;
   }
-  if (n_cur == 1 && l3_fwd_lds(f, in_w, in_h) <= kLdsCap) {
+  if (n_cur == 1 && l3_fwd_lds(f, in_w, in_h) <= kLdsMax) {
     const uint32_t grid = std::min<uint32_t>(batch, 1024);
     const size_t lds = l3_fwd_lds(f, in_w, in_h);
 #define SRCNN_L3_F(N2, F3)                                                                      \
     if (n_prev == N2 && f == F3) {                                                              \
+      if (int rc = set_lds(l3_fwd_kernel<N2, F3>, lds)) return rc;                              \
       SRCNN_PROFILE("conv_fwd_l3_mfma", s);                                                     \
       hipLaunchKernelGGL((l3_fwd_kernel<N2, F3>), dim3(grid), dim3(256), lds, s, in, W, B, out, \
                          (int)in_w, (int)in_h, (int)batch, relu);                               \

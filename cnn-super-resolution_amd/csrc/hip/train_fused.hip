@@ -23,6 +23,8 @@
 // layer-by-layer dataflow.  Results are deterministic: the
 // sample -> block -> wave assignment is static and every sum has a fixed
 // order; no float atomics anywhere.
+#include <algorithm>
+
 #include "common.hpp"
 #include "mfma.hpp"
 #include "ops.hpp"
@@ -857,19 +859,32 @@ static int launch_l3(const float* A2, const float* T, const float* W3, const flo
 template <int N1, int N2, int F1, int F3>
 static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t batch,
                const float* params, float* grads, float* sq_err, float* A1, float* A2, float* D2,
-               float* slab, size_t slab_bytes, hipStream_t s, bool query_only, size_t* need) {
+               float* A3, float* D3, float* slab, size_t slab_bytes, hipStream_t s, bool query_only,
+               size_t* need) {
   using NetT = Net<N1, N2, F1, F3>;
   const int ow = w - F1 + 1, oh = h - F1 + 1;
   const int w3 = ow - F3 + 1, h3 = oh - F3 + 1;
   if ((int)(w * h) > kXsMax || (int)w > kL12S || (int)h > kL12Rows || w3 <= 0 || h3 <= 0) return 0;
+  // l3_delta holds two A2 tiles in LDS: up to 640 A2 pixels (33x33 tiles at
+  // f1 = 9).  Larger tiles (e.g. the reference's 36x36 samples, profile.py:7)
+  // keep l12 and d1 and run layer 3 through the op-level kernels instead
+  // (ops_fast.hip: L3 forward, last delta, delta2, gW3 over HWC A2 / A3 / D3).
   const size_t lds3 = l3_lds_bytes<N2, F3>(ow, oh);
-  if (lds3 > 160 * 1024 || w3 * h3 > kL3MaxOut) return 0;
-  if (((ow * oh + 15) / 16 + kL3Threads / 64 - 1) / (kL3Threads / 64) > L3Lds<N2, F3>::kUnitsPerWave) return 0;
+  const bool l3_fused =
+      lds3 <= 160 * 1024 && w3 * h3 <= kL3MaxOut &&
+      ((ow * oh + 15) / 16 + kL3Threads / 64 - 1) / (kL3Threads / 64) <= L3Lds<N2, F3>::kUnitsPerWave;
   const int g12 = grid_for_batch(batch, SRCNN_L12_GRID);
   const int g3 = grid_for_batch(batch, 256);
   const int gd = grid_for_batch(batch, 512);
-  const size_t s12 = (size_t)gd * NetT::P12, s3 = (size_t)g3 * NetT::P3;
-  const size_t bytes = (s12 + s3 + g3) * sizeof(float);
+  const size_t s12 = (size_t)gd * NetT::P12;
+  size_t s3 = (size_t)g3 * NetT::P3, ssq = g3;  // gW3 slabs, squared-error slabs
+  if (!l3_fused) {  // the op-level gW3 slabs; the same space serves the squared-error reduction
+    s3 = fast::grad_workspace_bytes(N2, 1, F3, w3, h3, batch) / sizeof(float);
+    if (s3 == 0) return 0;  // the op-level layer-3 kernels do not take this tile either
+    s3 = std::max<size_t>(s3, reduce_blocks((size_t)batch * w3 * h3) + 1);
+    ssq = 0;
+  }
+  const size_t bytes = (s12 + s3 + ssq) * sizeof(float);
   if (query_only) {
     *need = bytes;
     return 1;
@@ -894,10 +909,24 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
     SRCNN_LAUNCH_TRY();
   }
   L3Geom lg{(int)w, (int)h, ow, oh, w3, h3, (int)batch};
-  {
+  if (l3_fused) {
     SRCNN_PROFILE("l3_delta_fused", s);
     int rc = launch_l3<N2, F3>(A2, T, W3, B3, D2, slab3, sqs, lg, g3, lds3, s);
     if (rc) return rc;
+  } else {
+    // ConfigBasedDataPipeline.cpp:200-323 for layer 3 on the op-level kernels
+    const int rf = fast::try_conv_fwd(A2, A3, W3, B3, ow, oh, N2, 1, F3, 0, batch, s);
+    if (rf != 1) return rf < 0 ? rf : fail(SRCNN_ERR_INVALID, "fused step: no layer-3 kernel for %dx%d", ow, oh);
+    if (sq_err)
+      if (int rc = reduce(2, A3, T, (size_t)batch * w3 * h3, w, h, w3, h3, sq_err, 1, slab3,
+                          s3 * sizeof(float), s))
+        return rc;
+    if (int rc = generic::last_delta(T, A3, D3, w, h, w3, h3, batch, s)) return rc;
+    const int rd = fast::try_conv_delta(D3, A2, D2, W3, F3, N2, 1, ow, oh, batch, s);
+    if (rd != 1) return rd < 0 ? rd : fail(SRCNN_ERR_INVALID, "fused step: no delta2 kernel for %dx%d", ow, oh);
+    const int rg = fast::try_conv_grad_acc(A2, D3, grads + NetT::P12, grads + NetT::P12 + NetT::P3 - 1, N2, 1,
+                                           F3, w3, h3, batch, slab3, s3 * sizeof(float), s);
+    if (rg != 1) return rg < 0 ? rg : fail(SRCNN_ERR_INVALID, "fused step: no gW3 kernel for %dx%d", ow, oh);
   }
   {
     SRCNN_PROFILE("delta1_grad12_fused", s);
@@ -910,7 +939,7 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
     const SlabSeg segs[3] = {{slab12, grads, gd, NetT::P12, 0},
                              {slab3, grads + NetT::P12, g3, NetT::P3, 0},
                              {sqs, sq_err, g3, 1, 0}};
-    int rc = reduce_slabs(segs, sq_err ? 3 : 2, s);
+    int rc = l3_fused ? reduce_slabs(segs, sq_err ? 3 : 2, s) : reduce_slabs(segs, 1, s);
     if (rc) return rc;
   }
   return 1;
@@ -919,12 +948,13 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
 template <int N1, int N2, int F1, int F3>
 static int dispatch_one(const srcnn_net* net, const float* X, const float* T, uint32_t w,
                         uint32_t h, uint32_t batch, const float* params, float* grads,
-                        float* sq_err, float* A1, float* A2, float* D2, float* slab,
-                        size_t slab_bytes, hipStream_t s, bool query_only, size_t* need) {
+                        float* sq_err, float* A1, float* A2, float* D2, float* A3, float* D3,
+                        float* slab, size_t slab_bytes, hipStream_t s, bool query_only,
+                        size_t* need) {
   if (net->n1 != (uint32_t)N1 || net->n2 != (uint32_t)N2 || net->f1 != (uint32_t)F1 ||
       net->f2 != 1 || net->f3 != (uint32_t)F3)
     return 0;
-  return run<N1, N2, F1, F3>(X, T, w, h, batch, params, grads, sq_err, A1, A2, D2, slab,
+  return run<N1, N2, F1, F3>(X, T, w, h, batch, params, grads, sq_err, A1, A2, D2, A3, D3, slab,
                              slab_bytes, s, query_only, need);
 }
 
@@ -937,15 +967,17 @@ int train_clock(int slot, double* ghz) {
 
 int train_fwd_bwd(const srcnn_net* net, const float* X, const float* T, uint32_t w, uint32_t h,
                   uint32_t batch, const float* params, float* grads, float* sq_err, float* A1,
-                  float* A2, float* D2, float* slab, size_t slab_bytes, hipStream_t s,
-                  bool query_only, size_t* need) {
+                  float* A2, float* D2, float* A3, float* D3, float* slab, size_t slab_bytes,
+                  hipStream_t s, bool query_only, size_t* need) {
   int rc;
 #define SRCNN_FUSED_CASE(n1, n2, f1, f3)                                                         \
   if ((rc = dispatch_one<n1, n2, f1, f3>(net, X, T, w, h, batch, params, grads, sq_err, A1, A2,  \
-                                         D2, slab, slab_bytes, s, query_only, need)) != 0)       \
+                                         D2, A3, D3, slab, slab_bytes, s, query_only, need)) != 0) \
     return rc;
   SRCNN_FUSED_CASE(64, 32, 9, 5)  // reference default (BASELINE.json configs[1])
   SRCNN_FUSED_CASE(32, 16, 9, 5)  // example_config.json
+  SRCNN_FUSED_CASE(64, 32, 9, 3)  // the default / example nets with a 3x3 last layer
+  SRCNN_FUSED_CASE(32, 16, 9, 3)
 #undef SRCNN_FUSED_CASE
   return 0;
 }

@@ -343,16 +343,16 @@ def test_conv_grad_vs_oracle(S, path, shape):
 # network level (ConfigBasedDataPipeline) vs the oracle
 # ----------------------------------------------------------------------------
 NETS = {"default": (64, 32, 9, 1, 5), "wide": (128, 64, 9, 5, 5), "tiny": (8, 4, 5, 1, 3),
-        "example": (32, 16, 9, 1, 5)}
+        "example": (32, 16, 9, 1, 5), "default_f3": (64, 32, 9, 1, 3)}
 
 
 def expected_train_path(name, size, path):
     """Kernel family srcnn_train_fwd_bwd must report (srcnn_last_path): the
-    fused f2 == 1 kernels take tiles whose A2 (two ping-pong copies in l3's
-    160 KB LDS) has at most 640 pixels, i.e. up to 33x33 for f1 = 9."""
+    fused f2 == 1 kernels take tiles up to 39x39 (l12's and d1's LDS images);
+    past 33x33 layer 3 runs on the op-level kernels between them."""
     if path == 1:
         return {"generic"}
-    if name in ("default", "example") and (size - 8) ** 2 <= 640:
+    if name in ("default", "example", "default_f3") and size <= 39:
         return {"fused"}
     if name == "wide":
         return {"wide"}
@@ -365,8 +365,12 @@ def expected_train_path(name, size, path):
                                              # ragged against the grids: l3 (256 blocks, walks the
                                              # batch from its end), l12 / d1 (512 blocks)
                                              ("default", 257, 33), ("default", 513, 33),
-                                             # tiles past the fused kernels' limit (33x33)
-                                             ("default", 9, 36), ("example", 5, 39)])
+                                             # tiles past l3_delta's LDS image (33x33): l12 +
+                                             # op-level layer 3 + d1; 36x36 as the reference's
+                                             # train_samples36 (profile.py:7)
+                                             ("default", 9, 36), ("example", 5, 39),
+                                             ("default", 300, 36), ("default_f3", 7, 33),
+                                             ("default", 3, 40)])
 def test_train_step_vs_oracle(S, path, name, batch, size):
     cfg = NETS[name]
     net = S.Net(*cfg)

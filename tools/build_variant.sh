@@ -12,5 +12,5 @@ for f in $(cd $P/csrc/hip && ls *.cpp *.hip); do
     -Wno-unused-result -I$R/include -I$P/csrc/hip "$@" -x hip -c $P/csrc/hip/$f -o $O/$f.o &
 done
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $P/lib/variants/libsrcnn_hip_$name.so $O/*.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $P/lib/variants/libsrcnn_hip_$name.so $O/*.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 echo built $P/lib/variants/libsrcnn_hip_$name.so
