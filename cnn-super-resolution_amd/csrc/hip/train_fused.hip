@@ -354,7 +354,7 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
   // delta2 LDS image rows: SRCNN_D1_D2SW = 1: N2 floats, quads of row r
   // XOR-swizzled by d2sw(r) = (r >> 1) mod N2/4; 0: one pad quad per row
   constexpr int DS = kD1D2Sw ? N2 : N2 + 4;
-  constexpr int WS = N2 + 1;              // padded W2 row in LDS
+  constexpr int WS = N2 + 1;              // W2 image (N1 * N2 floats) within N1 * WS
   constexpr int NW1 = K1 * N1, NW2 = N1 * N2;
   constexpr int P12 = NW1 + N1 + NW2 + N2;  // [gW1 | gB1 | gW2 | gB2]
   static_assert(N2 % 4 == 0 && N1 % 32 == 0 && KR <= 4, "d1 tile shape");
@@ -387,9 +387,13 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
   // pixel counts here, so the truncation is an exact q / ow
   const float inv_ow = 1.0f / (float)g.ow;
 
+  // W2 as the delta1 B-operand image: [k-step s][lane][channel tile t] holds
+  // W2[c = 16t + lq][n = 4s + lg], so each k-step's NQ operands of a lane are
+  // one contiguous (conflict-free) 16-B read (NQ = 4) instead of NQ 2-way
+  // conflicted 4-B reads
   for (int i = threadIdx.x; i < N1 * N2; i += blockDim.x) {
-    const int c = i / N2, n = i - c * N2;
-    w2s[c * WS + n] = W2[i];
+    const int t = i % NQ, l = (i / NQ) % 64, sk = i / (NQ * 64);
+    w2s[i] = W2[(16 * t + (l & 15)) * N2 + 4 * sk + (l >> 4)];
   }
   // gW1 A-operand rows of this lane: taps 16m + lq
   int toff[MT];
@@ -552,8 +556,14 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
         for (int pm = 0; pm < 2; pm++)
           a[pm] = kD1DiagLinD1 ? d2me[lane + 64 * ((s + pm) & 7)]
                                : d2me[kD1D2Sw ? (dab ^ (4 * s)) + 16 * pm * DS : (16 * pm + lq) * DS + n];
+        if constexpr (NQ == 4) {
+          const f32x4 bv = *reinterpret_cast<const f32x4*>(w2s + (s * 64 + lane) * NQ);
 #pragma unroll
-        for (int t = 0; t < NQ; t++) b[t] = kD1DiagLinD1 ? w2s[lane + 64 * ((s + t) & 7)] : w2s[(16 * t + lq) * WS + n];
+          for (int t = 0; t < NQ; t++) b[t] = bv[t];
+        } else {
+#pragma unroll
+          for (int t = 0; t < NQ; t++) b[t] = w2s[(s * 64 + lane) * NQ + t];
+        }
 #pragma unroll
         for (int pm = 0; pm < 2; pm++)
 #pragma unroll
