@@ -335,6 +335,33 @@ def forward_4k(S, net_t, frames=5, warmup=2, w=3840, h=2160):
     return res
 
 
+def forward_tile_256(S, net_t, reps=20):
+    """BASELINE.json configs[0] on the GPU: one 256x256 luma tile through the
+    fused inference kernels (srcnn_forward), ms per tile, beside the CPU
+    restatement's time for the same tile (cpu_forward_baseline)."""
+    net = S.Net(*net_t)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    stream = torch.cuda.current_stream().cuda_stream
+    w = h = 256
+    rng = np.random.default_rng(256)
+    x = torch.from_numpy((rng.random(w * h, dtype=np.float32) - 0.5)).to(dev)
+    prm = torch.from_numpy(init_params(net_t, S.net_param_count(net))).to(dev)
+    pad = net_t[2] + net_t[3] + net_t[4] - 3
+    out = torch.empty((w - pad) * (h - pad), device=dev)
+    nbytes = S.forward_workspace_bytes(net, w, h, 1)
+    ws = torch.empty(nbytes // 4 + 64, device=dev)
+    for _ in range(3):
+        S.forward(net, x, w, h, 1, prm, out, ws, nbytes, stream)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        S.forward(net, x, w, h, 1, prm, out, ws, nbytes, stream)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / reps * 1e3
+    return {"tile": "256x256", "ms": round(ms, 4), "gflop_s": round(forward_flops(net_t, w, h) / (ms * 1e-3) / 1e9, 1),
+            "kernel_path": S.last_path(), "reps": reps}
+
+
 WIDE_NET = (128, 64, 9, 5, 5)
 
 
@@ -566,6 +593,7 @@ def main():
         }
         if world == 1 and not args.no_forward:
             out["forward"] = forward_4k(S, net_t)
+            out["forward_tile_256"] = forward_tile_256(S, net_t)
         if world == 1 and not args.no_wide:
             out["wide"] = wide_training(S)
         if world == 1 and not args.no_cpu_baseline:
