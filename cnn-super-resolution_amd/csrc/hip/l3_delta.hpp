@@ -73,8 +73,18 @@ struct L3Geom {
   int batch;
 };
 
-constexpr int kL3Threads = 512;
-constexpr int kL3TPF = 2;  // L3 outputs per thread (w3 * h3 <= kL3TPF * 512)
+#ifndef SRCNN_L3_THREADS
+#define SRCNN_L3_THREADS 512
+#endif
+constexpr int kL3Threads = SRCNN_L3_THREADS;
+constexpr int kL3TPF = (1024 + kL3Threads - 1) / kL3Threads;  // L3 outputs per thread (w3 * h3 <= 1024)
+// diagnostics builds: store delta2 from the delta2 phase instead of holding it
+// in registers until the next sample's Q phase
+#ifdef SRCNN_L3_DIRECT_D2
+constexpr bool kL3DirectD2 = true;
+#else
+constexpr bool kL3DirectD2 = false;
+#endif
 constexpr int kL3MaxOut = kL3TPF * kL3Threads;
 
 // float index of A2[p][n] in the swizzled LDS image
@@ -90,7 +100,7 @@ struct L3Lds {
   // 16-pixel units per wave of the largest A2 tile whose two regions fit the
   // 160 KB LDS (npx2 * max(N2, F3^2) <= 20480 floats)
   static constexpr int kMaxPx = 20480 / (N2 > F3 * F3 ? N2 : F3 * F3);
-  static constexpr int kUnitsPerWave = ((kMaxPx + 15) / 16 + 7) / 8;
+  static constexpr int kUnitsPerWave = ((kMaxPx + 15) / 16 + kL3Threads / 64 - 1) / (kL3Threads / 64);
   int region;  // one ping-pong region: max(A2 tile, Q of whole units, reduction scratch)
   int d3off;   // delta3 grid offset (F3-1) * (w2 + 1)
   int nd3;     // delta3 grid size (zero tail covers chunk overrun)
@@ -239,7 +249,7 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
 
   // masked delta2 of this wave's units (slot j = unit wave + 8j), held
   // until the next sample's Q phase; D2 rows past the sample are not stored
-  f32x4 d2k[kUMax][NT];
+  f32x4 d2k[kL3DirectD2 ? 1 : kUMax][NT];
   float* d2dst = D2;
   bool d2pend = false;
 #define SRCNN_L3_D2_STORE(J)                                                           \
@@ -298,7 +308,7 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
         for (int s = 0; s < KQ; s++)
 #pragma unroll
           for (int t = 0; t < TT; t++) acc[t] = mfma::mma16(av[s], wq[s][t], acc[t]);
-        SRCNN_L3_D2_STORE(j);
+        if (!kL3DirectD2) SRCNN_L3_D2_STORE(j);
         // Q[u0 + 4lg + i][tap = 16t + lq] (the region holds whole units: rows
         // past the sample are written too, never read)
 #pragma unroll
@@ -395,10 +405,24 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
 #pragma unroll
             for (int t = 0; t < NT; t++)
               gacc[t3][t] = mfma::mma16(ag[s][t3], bg[s][t], gacc[t3][t]);
+        if constexpr (kL3DirectD2) {
+          const int q_ = u0 + lq;
+          if (q_ < npx2 && !kL3DiagNoStore) {
+            float* dst_ = D2 + ((size_t)l3_order(sample, g.batch) * npx2 + q_) * N2 + 4 * lg;
 #pragma unroll
-        for (int t = 0; t < NT; t++)
+            for (int t = 0; t < NT; t++) {
+              f32x4 v;
 #pragma unroll
-          for (int i = 0; i < 4; i++) d2k[j][t][i] = mk[t][i] > 0.0f ? acc[t][i] : 0.0f;
+              for (int i = 0; i < 4; i++) v[i] = mk[t][i] > 0.0f ? acc[t][i] : 0.0f;
+              *reinterpret_cast<f32x4*>(dst_ + 16 * t) = v;
+            }
+          }
+        } else {
+#pragma unroll
+          for (int t = 0; t < NT; t++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) d2k[j][t][i] = mk[t][i] > 0.0f ? acc[t][i] : 0.0f;
+        }
       }
     }
     d2dst = D2 + (size_t)l3_order(sample, g.batch) * npx2 * N2;
@@ -406,8 +430,9 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
     SRCNN_L3_TICK(3);
     cur ^= 1;
   }
+  if (!kL3DirectD2)
 #pragma unroll
-  for (int j = 0; j < kUMax; j++) SRCNN_L3_D2_STORE(j);
+    for (int j = 0; j < kUMax; j++) SRCNN_L3_D2_STORE(j);
 #undef SRCNN_L3_D2_STORE
 #undef SRCNN_L3_A2_DMA
   SRCNN_CLOCK_END(g_clk, 1);

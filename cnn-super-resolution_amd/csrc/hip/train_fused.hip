@@ -338,6 +338,9 @@ constexpr bool kD1A1Sw = SRCNN_D1_A1SW;
 #define SRCNN_D1_TOPWAIT 1  // sample top waits for the X tile only, not the next chunk's operands
 #endif
 constexpr bool kD1TopWait = SRCNN_D1_TOPWAIT;
+#ifndef SRCNN_D1_DMA_STEPS
+#define SRCNN_D1_DMA_STEPS 8  // gW1 k-steps the next work item's operand DMA is spread over
+#endif
 template <int N1, int N2, int F1>
 __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
     const float* __restrict__ X, const float* __restrict__ A1, const float* __restrict__ D2,
@@ -645,7 +648,7 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
     const int y_ = (int)(((float)q_ + 0.5f) * inv_ow);                              \
     return q_ + y_ * (g.W - g.ow);                                                  \
   }())
-        constexpr int kDmaPerStep = (kDmaK + 7) / 8;
+        constexpr int kDmaPerStep = (kDmaK + SRCNN_D1_DMA_STEPS - 1) / SRCNN_D1_DMA_STEPS;
         float acur[MT], rcur[KR > 0 ? KR : 1];
         {
           const int xb = SRCNN_D1_XB(0);
