@@ -362,6 +362,42 @@ def forward_tile_256(S, net_t, reps=20):
             "kernel_path": S.last_path(), "reps": reps}
 
 
+def forward_4k_sharded(S, net_t, rank, world, reduce_max, frames=10, warmup=3, w=3840, h=2160):
+    """BASELINE.json configs[4] on N GPUs: the 3840x2160 frame sharded by row
+    bands with a 12-row halo (parallel.forward_band), no
+    collective in the data path.  Every rank holds the frame and writes its
+    band of the output; Mpix/s of the whole frame over the slowest rank."""
+    from srcnn_amd import parallel
+    net = S.Net(*net_t)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    stream = torch.cuda.current_stream().cuda_stream
+    rng = np.random.default_rng(4)
+    x = torch.from_numpy((rng.random(w * h, dtype=np.float32) - 0.5)).to(dev)
+    prm = torch.from_numpy(init_params(net_t, S.net_param_count(net))).to(dev)
+    ctx = net_t[2] + net_t[3] + net_t[4] - 3
+    out = torch.empty((w - ctx) * (h - ctx), device=dev)
+    _, ni, _, _ = parallel.frame_band(w, h, net_t[2:], rank, world)
+    nbytes = S.forward_workspace_bytes(net, w, max(ni, ctx + 1), 1)
+    ws = torch.empty(nbytes // 4 + 64, device=dev)
+    for _ in range(warmup):
+        parallel.forward_band(S, net, x, w, h, prm, out, ws, nbytes, stream, rank, world)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(frames):
+        parallel.forward_band(S, net, x, w, h, prm, out, ws, nbytes, stream, rank, world)
+    torch.cuda.synchronize()
+    dist.barrier()
+    el = reduce_max(time.perf_counter() - t0)
+    ms = el / frames * 1e3
+    return {"frame": "%dx%d" % (w, h), "frames": frames, "ms_per_frame": round(ms, 4),
+            "mpix_s": round(w * h / (ms * 1e-3) / 1e6, 1),
+            "tflops": round(forward_flops(net_t, w, h) / (ms * 1e-3) / 1e12, 2),
+            "sharding": "row bands of %d output rows + %d halo rows per GPU, no collective"
+                        % (-(-(h - ctx) // world), ctx),
+            "n_gpus": world, "kernel_path": S.last_path()}
+
+
 WIDE_NET = (128, 64, 9, 5, 5)
 
 
@@ -535,6 +571,13 @@ def main():
         elapsed = float(e.item())
     stats = S.profile_stats()
     assert np.isfinite(params.cpu().numpy()).all(), "non-finite parameters after training"
+    fwd_sharded = None
+    if world > 1 and not args.no_forward:
+        def reduce_max(v):
+            t = torch.tensor([v], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            return float(t.item())
+        fwd_sharded = forward_4k_sharded(S, net_t, rank, world, reduce_max)
 
     if rank == 0:
         K = args.steps
@@ -591,6 +634,8 @@ def main():
             "profiled_steps": n_prof,
             "cpu_baseline": None,
         }
+        if fwd_sharded is not None:
+            out["forward"] = fwd_sharded
         if world == 1 and not args.no_forward:
             out["forward"] = forward_4k(S, net_t)
             out["forward_tile_256"] = forward_tile_256(S, net_t)

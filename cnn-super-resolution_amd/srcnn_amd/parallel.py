@@ -23,7 +23,9 @@ The collective is injected too.  Two implementations:
   torch          dist.all_reduce on the process group (RCCL with backend
                  "nccl"; gloo in the CPU tests and the one-GPU rehearsal)
 """
+import contextlib
 import os
+import sys
 
 import torch
 import torch.distributed as dist
@@ -35,6 +37,21 @@ def env_world():
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
+@contextlib.contextmanager
+def _stdout_to_stderr():
+    """fd-level redirect: gloo prints its "[Gloo] Rank r is connected ..."
+    lines to stdout, where the bench's one JSON line must stand alone."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        yield
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
 def init(backend, device=None):
     """init_process_group from the env (MASTER_ADDR defaults to 127.0.0.1)."""
     rank, world, _ = env_world()
@@ -42,7 +59,9 @@ def init(backend, device=None):
         return rank, world
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     kw = {"device_id": device} if device is not None and backend == "nccl" else {}
-    dist.init_process_group(backend, rank=rank, world_size=world, **kw)
+    with _stdout_to_stderr():
+        dist.init_process_group(backend, rank=rank, world_size=world, **kw)
+        dist.barrier()  # gloo connects its mesh lazily on some versions
     return rank, world
 
 
@@ -54,6 +73,35 @@ def shard(global_batch, rank, world):
     base, rem = divmod(global_batch, world)
     start = rank * base + min(rank, rem)
     return start, base + (1 if rank < rem else 0)
+
+
+def frame_band(w, h, net_dims, rank, world):
+    """Row band of one frame for `rank` (inference shards by
+    spatial tile with a halo and needs no collective).  The output rows of the
+    valid convolution [0, h - ctx), ctx = f1 + f2 + f3 - 3 (the 12-row halo of
+    the default net), are split contiguously as `shard` splits tiles; the
+    band's input rows are its output rows plus ctx rows of context below.
+    Rows are contiguous in the row-major frame, so a band is a plain slice of
+    the input and output buffers: (in_row0, in_rows, out_row0, out_rows)."""
+    f1, f2, f3 = net_dims
+    ctx = f1 + f2 + f3 - 3
+    if w <= ctx or h <= ctx:
+        raise ValueError("frame smaller than the network's receptive field")
+    o0, n = shard(h - ctx, rank, world)
+    return o0, (n + ctx) if n else 0, o0, n
+
+
+def forward_band(S, net, X, w, h, params, out, ws, ws_bytes, stream, rank, world):
+    """srcnn_forward of this rank's row band of one w x h frame: X and out are
+    the whole frame's (flat, row-major) input and output tensors; only the
+    band's slices are read and written.  Returns the band's output row range."""
+    i0, ni, o0, no = frame_band(w, h, (net.f1, net.f2, net.f3), rank, world)
+    if no:
+        ctx = net.f1 + net.f2 + net.f3 - 3
+        ow = w - ctx
+        S.forward(net, X[i0 * w:(i0 + ni) * w], w, ni, 1, params, out[o0 * ow:(o0 + no) * ow], ws,
+                  ws_bytes, stream)
+    return o0, no
 
 
 class SrcnnComm:

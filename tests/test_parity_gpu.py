@@ -497,6 +497,41 @@ def test_forward_large_frame_fused_vs_generic(S):
     assert_close(res[1], ref, RTOL, "forward 1280x720 generic", ref64)
 
 
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_forward_row_bands_vs_oracle(S, world):
+    """Inference sharded by row bands (parallel.forward_band):
+    every rank's band run in turn on device 0 into one output buffer, each
+    band a slice of the frame's own buffers.  The stitched frame covers every
+    output and matches the oracle's whole-frame forward; the bands' region
+    grids start at their own row 0, so the sums are grouped differently from
+    the unsharded call (within RTOL of it, not bit-equal)."""
+    from srcnn_amd import parallel
+    cfg = NETS["default"]
+    net = S.Net(*cfg)
+    rng = np.random.default_rng(1000 + world)
+    w, h = 640, 365
+    X, _ = make_batch(rng, 1, w, h)
+    params = make_params(rng, cfg, sd=0.05)
+    n_out = (w - 12) * (h - 12)
+    nbytes = S.forward_workspace_bytes(net, w, h, 1)
+    ws = torch.empty(nbytes // 4 + 64, dtype=torch.float32, device="cuda")
+    Xd, Pd = D(X), D(params)
+    out = torch.full((n_out,), float("nan"), dtype=torch.float32, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    rows = 0
+    for r in range(world):
+        _, no = parallel.forward_band(S, net, Xd, w, h, Pd, out, ws, nbytes, stream, r, world)
+        rows += no
+    assert rows == h - 12
+    whole = torch.full((n_out,), float("nan"), dtype=torch.float32, device="cuda")
+    S.forward(net, Xd, w, h, 1, Pd, whole, ws, nbytes)
+    got = H(out)
+    assert np.isfinite(got).all()
+    ref = orc.forward(cfg, X, w, h, 1, params)
+    assert_close(got, ref, RTOL, "forward %d row bands" % world, orc.f64.forward(cfg, X, w, h, 1, params))
+    assert_close(got, H(whole), RTOL, "row bands vs whole frame")
+
+
 # ----------------------------------------------------------------------------
 # full size (BASELINE config 2: default net, 33x33, batch 4096)
 # ----------------------------------------------------------------------------
