@@ -19,11 +19,6 @@ void check(int rc, const char* what) {
   throw std::runtime_error(msg);
 }
 
-ImageData::ImageData(int w_, int h_, int bpp_, const unsigned char* px) : w(w_), h(h_), bpp(bpp_) {
-  data.assign(static_cast<size_t>(w) * h * bpp, 0);
-  if (px) std::memcpy(data.data(), px, data.size());
-}
-
 void RawMemoryHandle::release() {
   if (released) return;
   if (!is_view && ptr) srcnn_free(ptr);

@@ -12,6 +12,7 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <cstring>
 #include <ios>
 #include <memory>
 #include <stdexcept>
@@ -53,7 +54,10 @@ struct Event {
 /** Host image: w x h pixels of `bpp` bytes (reference opencl::utils::ImageData). */
 struct ImageData {
   ImageData() = default;
-  ImageData(int w, int h, int bpp, const unsigned char* px = nullptr);
+  ImageData(int w_, int h_, int bpp_, const unsigned char* px = nullptr) : w(w_), h(h_), bpp(bpp_) {
+    data.assign(static_cast<size_t>(w) * h * bpp, 0);
+    if (px) std::memcpy(data.data(), px, data.size());
+  }
   int w = 0, h = 0, bpp = 0;
   std::vector<unsigned char> data;
 };

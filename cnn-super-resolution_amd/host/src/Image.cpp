@@ -60,6 +60,7 @@ void decode_png(const std::vector<unsigned char>& f, ImageData& img) {
     if (pos + 12 + size_t(len) > f.size()) throw IOException("truncated PNG chunk");
     const unsigned char* d = &f[pos + 8];
     if (type == "IHDR") {
+      if (len < 13) throw IOException("short PNG IHDR");
       w = be32(d);
       h = be32(d + 4);
       depth = d[8];
@@ -81,6 +82,10 @@ void decode_png(const std::vector<unsigned char>& f, ImageData& img) {
   if (interlace) throw IOException("interlaced PNG is not supported");
   int ch = ctype == 0 ? 1 : ctype == 2 ? 3 : ctype == 3 ? 1 : ctype == 4 ? 2 : ctype == 6 ? 4 : 0;
   if (!ch) throw IOException("unsupported PNG color type");
+  check_dims(w, h, ch);
+  // zlib's deflate ratio is below 1032:1: IDAT data far too short for the
+  // raw size cannot inflate to it, so reject before allocating
+  if (idat.size() < (size_t(w) * ch + 1) * h / 1032) throw IOException("corrupt PNG image data");
   size_t stride = size_t(w) * ch;
   std::vector<unsigned char> raw((stride + 1) * h);
   uLongf out_len = raw.size();
@@ -148,7 +153,10 @@ void decode_pnm(const std::vector<unsigned char>& f, ImageData& img) {
   };
   int w = next_int(), h = next_int(), maxv = next_int();
   if (w <= 0 || h <= 0 || maxv != 255) throw IOException("unsupported PNM header");
-  size_t off = size_t(ss.tellg()) + 1;
+  check_dims(w, h, ch);
+  const std::streamoff pos = ss.tellg();
+  if (pos < 0) throw IOException("truncated PNM header");
+  size_t off = size_t(pos) + 1;
   if (off + size_t(w) * h * ch > f.size()) throw IOException("truncated PNM data");
   img = ImageData(w, h, ch, &f[off]);
 }
@@ -174,8 +182,13 @@ void convert(ImageData& img, int channels) {
 
 }  // namespace
 
-void load(const std::string& path, ImageData& img, int channels) {
-  auto f = read_all(path);
+void check_dims(uint64_t w, uint64_t h, int channels) {
+  if (w == 0 || h == 0 || w > kMaxImageSide || h > kMaxImageSide || w * h > kMaxImagePixels || channels < 1 ||
+      channels > 4)
+    throw IOException("unsupported image size " + std::to_string(w) + "x" + std::to_string(h));
+}
+
+void decode(const std::vector<unsigned char>& f, ImageData& img, int channels, const std::string& name) {
   if (f.size() >= 8 && f[0] == 137 && f[1] == 'P' && f[2] == 'N' && f[3] == 'G')
     decode_png(f, img);
   else if (f.size() >= 2 && f[0] == 'P' && (f[1] == '5' || f[1] == '6'))
@@ -183,9 +196,11 @@ void load(const std::string& path, ImageData& img, int channels) {
   else if (f.size() >= 3 && f[0] == 0xFF && f[1] == 0xD8 && f[2] == 0xFF)
     decode_jpeg(f, img);
   else
-    throw IOException("unsupported image format (JPEG / PNG / PNM only): " + path);
+    throw IOException("unsupported image format (JPEG / PNG / PNM only): " + name);
   convert(img, channels);
 }
+
+void load(const std::string& path, ImageData& img, int channels) { decode(read_all(path), img, channels, path); }
 
 void write(const std::string& path, const ImageData& img) {
   if (img.w <= 0 || img.h <= 0 || !(img.bpp == 1 || img.bpp == 3 || img.bpp == 4))

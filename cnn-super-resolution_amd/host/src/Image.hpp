@@ -12,6 +12,8 @@
 #ifndef SRCNN_HOST_IMAGE_HPP
 #define SRCNN_HOST_IMAGE_HPP
 
+#include <cstddef>
+#include <cstdint>
 #include <string>
 #include <vector>
 
@@ -23,6 +25,18 @@ namespace image {
 /** Load a JPEG, PNG or PNM file (by content) into `img`; `channels` 0 keeps
  * the file's channel count, 1/3/4 converts (gray <-> RGB, alpha = 255). */
 void load(const std::string& path, ImageData& img, int channels = 0);
+
+/** `load` on an in-memory file image; `name` only labels the error message. */
+void decode(const std::vector<unsigned char>& file, ImageData& img, int channels = 0,
+            const std::string& name = "<memory>");
+
+/** Largest decoded image, in pixels (and per side): corrupt or hostile
+ * headers must not turn into multi-GB allocations (16384 x 16384). */
+constexpr size_t kMaxImagePixels = size_t(1) << 28;
+constexpr uint32_t kMaxImageSide = 1u << 24;
+
+/** Throw IOException unless a w x h image with `channels` is within the caps. */
+void check_dims(uint64_t w, uint64_t h, int channels);
 
 /** Decode a JPEG file image (Jpeg.cpp) to 1 (gray) or 3 (RGB) channels. */
 void decode_jpeg(const std::vector<unsigned char>& file, ImageData& img);

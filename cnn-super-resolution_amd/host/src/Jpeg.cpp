@@ -32,6 +32,7 @@
 #include <vector>
 
 #include "Context.hpp"
+#include "Image.hpp"
 
 namespace srcnn {
 namespace image {
@@ -62,6 +63,7 @@ struct Huffman {
       valptr[len] = k;
       mincode[len] = code;
       for (int i = 0; i < counts[len - 1]; ++i, ++k, ++code) {
+        if (code >= (1 << len)) bad("bad Huffman table");  // over-subscribed code lengths
         if (len <= 9) {
           const int shift = 9 - len;
           for (int f = code << shift; f < ((code + 1) << shift); ++f)
@@ -161,6 +163,7 @@ class Decoder {
   void read_adobe() {
     const size_t start = pos_;
     const int len = u16();
+    if (len < 2) bad("bad segment length");
     if (len >= 14 && pos_ + 5 <= f_.size() && std::memcmp(&f_[pos_], "Adobe", 5) == 0)
       adobe_transform_ = f_[start + 13];
     pos_ = start + len;
@@ -218,6 +221,11 @@ class Decoder {
       hmax_ = std::max(hmax_, c.h);
       vmax_ = std::max(vmax_, c.v);
     }
+    check_dims(width_, height_, nc);
+    // every 8x8 luma block costs at least one bit of entropy-coded data (its DC
+    // code), so a file much smaller than that cannot hold the image: reject it
+    // before allocating the coefficient planes
+    if (f_.size() < (size_t(width_) * height_ / 64) / 64) bad("file too small for its frame size");
     mcux_ = (width_ + 8 * hmax_ - 1) / (8 * hmax_);
     mcuy_ = (height_ + 8 * vmax_ - 1) / (8 * vmax_);
     for (auto& c : comp_) {
@@ -307,7 +315,7 @@ class Decoder {
   // ---- block decoders (coefficients in natural order, quantised) ----
   void block_baseline(Component& c, int16_t* blk) {
     const int t = decode_huff(dc_[c.dc_tab]);
-    c.dc_pred += receive_extend(t);
+    c.dc_pred = int(uint32_t(c.dc_pred) + uint32_t(receive_extend(t)));  // wraps on corrupt data
     blk[0] = int16_t(c.dc_pred);
     for (int k = 1; k < 64;) {
       const int rs = decode_huff(ac_[c.ac_tab]);
@@ -324,8 +332,8 @@ class Decoder {
   }
   void block_dc_first(Component& c, int16_t* blk, int al) {
     const int t = decode_huff(dc_[c.dc_tab]);
-    c.dc_pred += receive_extend(t);
-    blk[0] = int16_t(c.dc_pred * (1 << al));
+    c.dc_pred = int(uint32_t(c.dc_pred) + uint32_t(receive_extend(t)));
+    blk[0] = int16_t(int64_t(c.dc_pred) * (int64_t(1) << al));
   }
   void block_dc_refine(int16_t* blk, int al) {
     if (bit()) blk[0] = int16_t(blk[0] | (1 << al));
