@@ -1,21 +1,33 @@
 // codec_fuzz -- deterministic mutation fuzzing of the host's file parsers,
 // for the sanitizer build (tools/sanitize_host.sh: g++ -fsanitize=address,
 // undefined): the JPEG / PNG / PNM decoders (srcnn::image::decode, the data
-// path of `cnn train -i DIR` and `cnn dry -i IMAGE`) and the JSON reader of
-// config.json / parameters.json (srcnn::json::parse).  Every mutated input
-// must decode or throw; a crash, a hang or a sanitizer report is a failure.
+// path of `cnn train -i DIR` and `cnn dry -i IMAGE`), the JSON reader of
+// config.json / parameters.json (srcnn::json::parse) and the config.json
+// validation on top of it (cnn_sr::ConfigReader).  Every mutated input must
+// decode or throw; a crash, a hang or a sanitizer report is a failure.
 //   codec_fuzz [--iters N] [--seed S] FILE...
 // Prints one summary line per seed file: mutations tried / decoded / rejected.
+#include <unistd.h>
+
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
 #include <fstream>
 #include <iostream>
 #include <iterator>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
+#include "Config.hpp"
 #include "Image.hpp"
 #include "Json.hpp"
+
+// Context.cpp's srcnn::require (the harness links only the parsers, not the
+// device-facing host library)
+void srcnn::require(bool cond, const std::string& msg) {
+  if (!cond) throw std::runtime_error(msg);
+}
 
 namespace {
 
@@ -82,11 +94,18 @@ bool is_json(const std::vector<unsigned char>& f) {
   return false;
 }
 
+std::string g_tmp;  // config files go through ConfigReader::read(path)
+
 // true: decoded, false: rejected with an exception
 bool run_one(const std::vector<unsigned char>& m, bool json) {
   try {
     if (json) {
-      srcnn::json::parse(std::string(m.begin(), m.end()));
+      const std::string text(m.begin(), m.end());
+      const srcnn::json::Value v = srcnn::json::parse(text);
+      if (v.find("n1") || v.find("parameters_file")) {  // a config.json: validate it too
+        std::ofstream(g_tmp, std::ios::binary) << text;
+        cnn_sr::ConfigReader().read(g_tmp.c_str());
+      }
     } else {
       srcnn::ImageData img;
       srcnn::image::decode(m, img);
@@ -113,6 +132,7 @@ int main(int argc, char** argv) {
     else if (a == "--seed" && i + 1 < argc) seed = std::stoull(argv[++i]);
     else files.push_back(a);
   }
+  g_tmp = "/tmp/codec_fuzz_" + std::to_string(::getpid()) + ".json";
   if (files.empty()) {
     std::cerr << "usage: codec_fuzz [--iters N] [--seed S] FILE..." << std::endl;
     return 2;
@@ -140,5 +160,6 @@ int main(int argc, char** argv) {
     std::cout << files[fi] << " " << (json ? "json" : "image") << " mutations=" << iters << " decoded=" << ok
               << " rejected=" << rejected << std::endl;
   }
+  std::remove(g_tmp.c_str());
   return 0;
 }

@@ -10,7 +10,7 @@ H=$R/cnn-super-resolution_amd/host
 O=${SANITIZE_OUT:-$R/cnn-super-resolution_amd/build/sanitize}
 mkdir -p "$O"
 g++ -std=c++17 -O1 -g -fno-omit-frame-pointer -fsanitize=address,undefined -fno-sanitize-recover=all \
-  -I"$R/include" -I"$H/src" "$H/test/codec_fuzz.cpp" "$H/src/Image.cpp" "$H/src/Jpeg.cpp" "$H/src/Json.cpp" \
+  -I"$R/include" -I"$H/src" "$H/test/codec_fuzz.cpp" "$H/src/Image.cpp" "$H/src/Jpeg.cpp" "$H/src/Json.cpp" "$H/src/Config.cpp" \
   -o "$O/codec_fuzz" -lz
 args=()
 seeds=()
