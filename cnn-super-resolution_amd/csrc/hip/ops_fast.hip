@@ -239,13 +239,55 @@ __global__ __launch_bounds__(256) void pw_grad_kernel(const float* __restrict__ 
 }
 
 // ===========================================================================
-// layer 1 forward (n_prev == 1): A1 = act(B1 + conv(X, W1)), per sample
+// layer 1 forward (n_prev == 1): A1 = act(B1 + conv(X, W1)), per work item
 // GEMM M = pixels (32-row tiles, two per wave pass), N = 32 channels, K =
 // taps; the k-slot pairing gives half h the taps [KP h, KP h + KP), so every
 // operand read is a per-half base + an immediate.
+// A work item is one window of an image: up to (kXS - F1 + 1)^2 output pixels
+// whose kXS x kXS input window sits in LDS, so any image size runs here (a
+// 33x33 training tile is one window; a 256x256 image 64 of them).
 // ===========================================================================
-constexpr int kXS = 40;                    // LDS row stride of an input tile (w, h <= kXS)
+constexpr int kXS = 40;                    // LDS row stride of an input window
 constexpr int kXTile = kXS * (kXS + 1);    // + one zero row read by the padded tap
+
+// window geometry of work item `it` over `batch` images of w x h inputs
+struct L1Win {
+  int s, x0, y0, ow, oh;  // image, output window origin and size
+  __device__ L1Win(long long it, int w1, int h1, int wo) {
+    const int nwx = (w1 + wo - 1) / wo, nwin = nwx * ((h1 + wo - 1) / wo);
+    s = nwin == 1 ? (int)it : (int)(it / nwin);
+    const int wi = (int)(it - (long long)s * nwin), wy = wi / nwx;
+    x0 = (wi - wy * nwx) * wo;
+    y0 = wy * wo;
+    ow = min(wo, w1 - x0);
+    oh = min(wo, h1 - y0);
+  }
+};
+__host__ __device__ inline long long l1_items(int w1, int h1, int wo, int batch) {
+  return (long long)batch * ((w1 + wo - 1) / wo) * ((h1 + wo - 1) / wo);
+}
+
+// pixel p of a window of width ow -> its offset in an image of width wfull
+// from the window origin (no division when the window spans the image width,
+// as every training tile does)
+__device__ __forceinline__ int win_px(int p, int ow, int wfull) {
+  if (ow == wfull) return p;
+  const int y = p / ow;
+  return y * wfull + p - y * ow;
+}
+
+// X window of `win` -> xs (rows at stride kXS), and a zero row below it for
+// the padded tap; the caller brackets it with barriers
+template <int F1>
+__device__ void stage_x_window(const float* __restrict__ X, float* xs, const L1Win& win, int w, int h) {
+  const int iw = win.ow + F1 - 1, ih = win.oh + F1 - 1;
+  const float* src = X + (size_t)win.s * w * h + (size_t)win.y0 * w + win.x0;
+  for (int i = threadIdx.x; i < iw * ih; i += blockDim.x) {
+    const int y = i / iw;
+    xs[y * kXS + i - y * iw] = src[(size_t)y * w + i - y * iw];
+  }
+  for (int i = threadIdx.x; i < kXS; i += blockDim.x) xs[ih * kXS + i] = 0.0f;
+}
 
 template <int N1, int F1>
 __global__ __launch_bounds__(256) void l1_fwd_kernel(const float* __restrict__ X,
@@ -270,24 +312,23 @@ __global__ __launch_bounds__(256) void l1_fwd_kernel(const float* __restrict__ X
   const float bias = B1[n];
   for (int i = threadIdx.x; i < kXTile; i += 256) xs[i] = 0.0f;
   const int w1 = w - F1 + 1, h1 = h - F1 + 1;
-  const int npx = w1 * h1, mtiles = (npx + 31) / 32;
+  constexpr int WO = kXS - F1 + 1;
+  const long long items = l1_items(w1, h1, WO, batch);
   // tap kp + KP (half 1) sits at one of two fixed offsets from tap kp
   const int dA = hh * (Q * kXS + R), dB = hh * ((Q + 1) * kXS + R - F1);
-  for (int s = blockIdx.x; s < batch; s += gridDim.x) {
+  for (long long it = blockIdx.x; it < items; it += gridDim.x) {
+    const L1Win win(it, w1, h1, WO);
+    const int npx = win.ow * win.oh, mtiles = (npx + 31) / 32;
     __syncthreads();
-    const float* xsrc = X + (size_t)s * w * h;
-    for (int i = threadIdx.x; i < w * h; i += 256) {
-      const int y = i / w;
-      xs[y * kXS + i - y * w] = xsrc[i];
-    }
+    stage_x_window<F1>(X, xs, win, w, h);
     __syncthreads();
-    float* dst = A1 + (size_t)s * npx * N1 + n;
+    float* dst = A1 + ((size_t)win.s * w1 * h1 + (size_t)win.y0 * w1 + win.x0) * N1 + n;
     for (int m = 2 * mg; m < mtiles; m += 2 * MG) {
       int base[2];
 #pragma unroll
       for (int u = 0; u < 2; u++) {
-        const int o = min(32 * (m + u) + j, npx - 1), oy = o / w1;
-        base[u] = oy * kXS + o - oy * w1;
+        const int o = min(32 * (m + u) + j, npx - 1), oy = o / win.ow;
+        base[u] = oy * kXS + o - oy * win.ow;
       }
       f32x16 acc0 = zero16(), acc1 = zero16();
 #pragma unroll
@@ -297,12 +338,22 @@ __global__ __launch_bounds__(256) void l1_fwd_kernel(const float* __restrict__ X
         acc0 = mma(xs[base[0] + dd + toff], wb[kp], acc0);
         acc1 = mma(xs[base[1] + dd + toff], wb[kp], acc1);
       }
+      if (win.ow == w1) {  // the window spans the image rows: pixel offsets as they are
 #pragma unroll
-      for (int r = 0; r < 16; r++) {
-        const int p0 = 32 * m + crow(r, hh), p1 = p0 + 32;
-        const float v0 = acc0[r] + bias, v1 = acc1[r] + bias;
-        if (p0 < npx) dst[(size_t)p0 * N1] = relu ? fmaxf(v0, 0.0f) : v0;
-        if (p1 < npx) dst[(size_t)p1 * N1] = relu ? fmaxf(v1, 0.0f) : v1;
+        for (int r = 0; r < 16; r++) {
+          const int p0 = 32 * m + crow(r, hh), p1 = p0 + 32;
+          const float v0 = acc0[r] + bias, v1 = acc1[r] + bias;
+          if (p0 < npx) dst[(size_t)p0 * N1] = relu ? fmaxf(v0, 0.0f) : v0;
+          if (p1 < npx) dst[(size_t)p1 * N1] = relu ? fmaxf(v1, 0.0f) : v1;
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+          const int p0 = 32 * m + crow(r, hh), p1 = p0 + 32;
+          const float v0 = acc0[r] + bias, v1 = acc1[r] + bias;
+          if (p0 < npx) dst[(size_t)win_px(p0, win.ow, w1) * N1] = relu ? fmaxf(v0, 0.0f) : v0;
+          if (p1 < npx) dst[(size_t)win_px(p1, win.ow, w1) * N1] = relu ? fmaxf(v1, 0.0f) : v1;
+        }
       }
     }
   }
@@ -336,7 +387,9 @@ __global__ __launch_bounds__(256, 1) void l1_grad_kernel(const float* __restrict
   __shared__ float red[MT * CT * 4 * 64];
   const int lane = lane_id(), wave = wave_id(), lq = lane & 15, lg = lane >> 4;
   const int cg = wave / WPG, ws = wave % WPG;  // channel group, pixel slice
-  const int w1 = w - F1 + 1, h1 = h - F1 + 1, npx = w1 * h1;
+  const int w1 = w - F1 + 1, h1 = h - F1 + 1;
+  constexpr int WO = kXS - F1 + 1;
+  const long long items = l1_items(w1, h1, WO, batch);
   // per-lane tap offsets of rows 16m + lq; the ones row / pad rows read fixed slots
   int toff[MT];
 #pragma unroll
@@ -349,29 +402,29 @@ __global__ __launch_bounds__(256, 1) void l1_grad_kernel(const float* __restrict
   for (int m = 0; m < MT; m++)
 #pragma unroll
     for (int t = 0; t < CT; t++) acc[m][t] = zero4();
-  const int ngrp = (npx + 3) / 4;
-  for (int s = blockIdx.x; s < batch; s += gridDim.x) {
+  for (long long it = blockIdx.x; it < items; it += gridDim.x) {
+    const L1Win win(it, w1, h1, WO);
+    const int npx = win.ow * win.oh, ngrp = (npx + 3) / 4;
     __syncthreads();
-    const float* xsrc = X + (size_t)s * w * h;
-    for (int i = threadIdx.x; i < w * h; i += 256) {
-      const int y = i / w;
-      xs[y * kXS + i - y * w] = xsrc[i];
-    }
+    stage_x_window<F1>(X, xs, win, w, h);
     __syncthreads();
-    const float* ds = D + (size_t)s * npx * N1 + 16 * CT * cg + lq;
+    const float* ds = D + ((size_t)win.s * w1 * h1 + (size_t)win.y0 * w1 + win.x0) * N1 + 16 * CT * cg + lq;
     float bn[CT];  // the next group's delta operands (HBM), in flight under the MFMAs
     auto load_b = [&](int gq) {
       const int p = 4 * gq + lg;
-      const int pc = min(p, npx - 1);
+      const size_t q = win_px(min(p, npx - 1), win.ow, w1);  // window pixel -> image pixel
 #pragma unroll
-      for (int t = 0; t < CT; t++) bn[t] = p < npx ? ds[(size_t)pc * N1 + 16 * t] : 0.0f;
+      for (int t = 0; t < CT; t++) bn[t] = p < npx ? ds[q * N1 + 16 * t] : 0.0f;
     };
     if (ws < ngrp) load_b(ws);
+    // window pixel p = 4gq + lg as (row py, column px), advanced by 4 WPG
+    // pixels per step without a division
+    int py = (4 * ws + lg) / win.ow, px = 4 * ws + lg - py * win.ow;
     for (int gq = ws; gq < ngrp; gq += WPG) {
       const int p = 4 * gq + lg;
       const bool ok = p < npx;
-      const int pc = ok ? p : npx - 1;
-      const int py = pc / w1, xb = py * kXS + pc - py * w1;
+      const int xb = ok ? py * kXS + px : 0;  // (rows past the window: delta operand 0)
+      for (px += 4 * WPG; px >= win.ow; px -= win.ow) ++py;
       float bv[CT];
 #pragma unroll
       for (int t = 0; t < CT; t++) bv[t] = bn[t];
@@ -417,16 +470,19 @@ __global__ __launch_bounds__(256, 1) void l1_grad_kernel(const float* __restrict
 // ===========================================================================
 // layer 3 (single output channel), per sample
 // ===========================================================================
-// Q[q][tap] for q < npx_in: M = taps (16-row tiles), N = 16 pixels, K = channels
-// with 16-B operand loads of the input straight from HBM (see pw_kernel)
+// Q[q][tap] for the A2 pixels q of a window: M = taps (16-row tiles), N = 16
+// pixels, K = channels with 16-B operand loads of the input straight from HBM
+// (see pw_kernel).  A work item is a window of up to wo x wo outputs (the
+// L1Win geometry over the A3 grid) whose (wo + F3 - 1)^2 A2 pixels' Q rows sit
+// in LDS; a training tile is one window, any larger image several.
 template <int N2, int F3>
 __global__ __launch_bounds__(256) void l3_fwd_kernel(const float* __restrict__ A2,
                                                      const float* __restrict__ W3,
                                                      const float* __restrict__ B3,
                                                      float* __restrict__ A3, int w2, int h2,
-                                                     int batch, int relu) {
+                                                     int batch, int relu, int wo) {
   constexpr int K3 = F3 * F3, TT = (K3 + 15) / 16, KJ = N2 / 16;
-  extern __shared__ __attribute__((aligned(16))) float qs[];  // [npx2][K3]
+  extern __shared__ __attribute__((aligned(16))) float qs[];  // [window A2 pixels][K3]
   const int lane = lane_id(), wave = wave_id(), lq = lane & 15, lg = lane >> 4;
   // A operand of k-step (j, i): W3[tap = 16t + lq][c = 16j + 4lg + i]
   float wq[KJ][4][TT];
@@ -440,15 +496,17 @@ __global__ __launch_bounds__(256) void l3_fwd_kernel(const float* __restrict__ A
         wq[j][i][t] = tap < K3 ? W3[tap * N2 + 16 * j + 4 * lg + i] : 0.0f;
       }
   const float b3 = B3[0];
-  const int npx2 = w2 * h2, nunit = (npx2 + 15) / 16;
-  const int w3 = w2 - F3 + 1, h3 = h2 - F3 + 1, nout = w3 * h3;
-  for (int s = blockIdx.x; s < batch; s += gridDim.x) {
-    const float* src = A2 + (size_t)s * npx2 * N2;
+  const int w3 = w2 - F3 + 1, h3 = h2 - F3 + 1;
+  const long long items = l1_items(w3, h3, wo, batch);
+  for (long long it = blockIdx.x; it < items; it += gridDim.x) {
+    const L1Win win(it, w3, h3, wo);
+    const int iw = win.ow + F3 - 1, npxw = iw * (win.oh + F3 - 1), nunit = (npxw + 15) / 16;
+    const float* src = A2 + ((size_t)win.s * w2 * h2 + (size_t)win.y0 * w2 + win.x0) * N2;
     f32x4 xn[KJ];  // the next unit's operands, in flight under this unit's MFMAs
     auto load_x = [&](int u) {
-      const int q = min(16 * u + lq, npx2 - 1);
+      const size_t g = win_px(min(16 * u + lq, npxw - 1), iw, w2);  // window pixel -> image pixel
 #pragma unroll
-      for (int j = 0; j < KJ; j++) xn[j] = *reinterpret_cast<const f32x4*>(src + (size_t)q * N2 + 16 * j + 4 * lg);
+      for (int j = 0; j < KJ; j++) xn[j] = *reinterpret_cast<const f32x4*>(src + g * N2 + 16 * j + 4 * lg);
     };
     if (wave < nunit) load_x(wave);
     for (int u = wave; u < nunit; u += kWaves) {
@@ -466,7 +524,7 @@ __global__ __launch_bounds__(256) void l3_fwd_kernel(const float* __restrict__ A
 #pragma unroll
           for (int t = 0; t < TT; t++) acc[t] = mma16(wq[j][i][t], x[j][i], acc[t]);
       // lane (lq, lg) reg i: Q[16u + lq][tap = 16t + 4lg + i]
-      if (16 * u + lq < npx2)
+      if (16 * u + lq < npxw)
 #pragma unroll
         for (int t = 0; t < TT; t++)
 #pragma unroll
@@ -476,33 +534,46 @@ __global__ __launch_bounds__(256) void l3_fwd_kernel(const float* __restrict__ A
           }
     }
     __syncthreads();
-    float* dst = A3 + (size_t)s * nout;
-    for (int p = threadIdx.x; p < nout; p += blockDim.x) {
-      const int y = p / w3, x = p - y * w3;
-      const float* qrow = qs + (y * w2 + x) * K3;
+    float* dst = A3 + (size_t)win.s * w3 * h3 + (size_t)win.y0 * w3 + win.x0;
+    for (int p = threadIdx.x; p < win.ow * win.oh; p += blockDim.x) {
+      const int y = p / win.ow, x = p - y * win.ow;
+      const float* qrow = qs + (y * iw + x) * K3;
       float acc = 0.0f;
 #pragma unroll
       for (int dy = 0; dy < F3; dy++)
 #pragma unroll
-        for (int dx = 0; dx < F3; dx++) acc += qrow[(dy * w2 + dx) * K3 + dy * F3 + dx];
+        for (int dx = 0; dx < F3; dx++) acc += qrow[(dy * iw + dx) * K3 + dy * F3 + dx];
       const float v = acc + b3;
-      dst[p] = relu ? fmaxf(v, 0.0f) : v;
+      dst[win_px(p, win.ow, w3)] = relu ? fmaxf(v, 0.0f) : v;
     }
     __syncthreads();
   }
 }
 
-// delta3 of sample s on the A2 grid with a zero border: d3g[q + d3off - off(tap)]
-// is delta3(q - off(tap)) for A2 pixel q (0 outside the A3 grid)
+// The delta2 / gW3 kernels work on windows of up to kD3Win x kD3Win A2 pixels
+// (L1Win over the A2 grid; a training tile is one window).  A window's delta3
+// neighbourhood is staged with a zero border as the grid G of row stride
+// gw = ow + F3 - 1: G[gy][gx] = delta3(y0 - (F3-1) + gy, x0 - (F3-1) + gx), 0
+// outside the A3 grid.  For window pixel (py, px) at g = py * gw + px,
+// delta3(A2 pixel - off(dy, dx)) is then G[g + d3off - (dy * gw + dx)] with
+// d3off = (F3 - 1)(gw + 1): one add per tap.
+constexpr int kD3Win = 64;
+
+// gb != nullptr: also add the delta3 values at the window's own A2 pixels
+// (gB3: every delta3 pixel is counted by exactly one window)
 template <int F3>
-__device__ void stage_d3(const float* __restrict__ D3, float* d3g, int s, int w2, int h2, int nd3) {
-  const int w3 = w2 - F3 + 1, h3 = h2 - F3 + 1, d3off = (F3 - 1) * (w2 + 1);
-  for (int i = threadIdx.x; i < nd3; i += blockDim.x) d3g[i] = 0.0f;
-  __syncthreads();
-  const float* src = D3 + (size_t)s * w3 * h3;
-  for (int i = threadIdx.x; i < w3 * h3; i += blockDim.x) {
-    const int y = i / w3, x = i - y * w3;
-    d3g[y * w2 + x + d3off] = src[i];
+__device__ void stage_d3_window(const float* __restrict__ D3, float* G, const L1Win& win, int w2, int h2,
+                                float* gb = nullptr) {
+  const int w3 = w2 - F3 + 1, h3 = h2 - F3 + 1;
+  const int gw = win.ow + F3 - 1, ng = gw * (win.oh + F3 - 1);
+  const float* src = D3 + (size_t)win.s * w3 * h3;
+  __syncthreads();  // the previous window's readers are done
+  for (int i = threadIdx.x; i < ng; i += blockDim.x) {
+    const int gy = i / gw, gx = i - gy * gw;
+    const int y = win.y0 - (F3 - 1) + gy, x = win.x0 - (F3 - 1) + gx;
+    const float v = (y >= 0 && y < h3 && x >= 0 && x < w3) ? src[(size_t)y * w3 + x] : 0.0f;
+    G[i] = v;
+    if (gb && gy >= F3 - 1 && gx >= F3 - 1) *gb += v;
   }
   __syncthreads();
 }
@@ -518,31 +589,35 @@ __global__ __launch_bounds__(256) void l3_delta_kernel(const float* __restrict__
   constexpr int K3 = F3 * F3, NQ = N2 / 4;
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* w3s = sm;            // [K3][N2]
-  float* d3g = sm + K3 * N2;  // delta3 grid
-  const int npx2 = w2 * h2, d3off = (F3 - 1) * (w2 + 1), nd3 = npx2 + d3off + 4;
+  float* d3g = sm + K3 * N2;  // delta3 window grid
   for (int i = threadIdx.x; i < K3 * N2; i += blockDim.x) w3s[i] = W3[i];
-  for (int s = blockIdx.x; s < batch; s += gridDim.x) {
-    stage_d3<F3>(D3, d3g, s, w2, h2, nd3);
-    const float* a2 = A2 + (size_t)s * npx2 * N2;
-    float* d2 = D2 + (size_t)s * npx2 * N2;
-    for (int e = threadIdx.x; e < npx2 * NQ; e += blockDim.x) {
-      const int q = e / NQ, cq = e - q * NQ;
+  const long long items = l1_items(w2, h2, kD3Win, batch);
+  for (long long it = blockIdx.x; it < items; it += gridDim.x) {
+    const L1Win win(it, w2, h2, kD3Win);
+    stage_d3_window<F3>(D3, d3g, win, w2, h2);
+    const int gw = win.ow + F3 - 1, d3off = (F3 - 1) * (gw + 1);
+    const size_t base = (size_t)win.s * w2 * h2 + (size_t)win.y0 * w2 + win.x0;
+    const float* a2 = A2 + base * N2;
+    float* d2 = D2 + base * N2;
+    for (int e = threadIdx.x; e < win.ow * win.oh * NQ; e += blockDim.x) {
+      const int p = e / NQ, cq = e - p * NQ, py = p / win.ow, px = p - py * win.ow;
+      const int g = py * gw + px;                 // window grid pixel
+      const size_t q = (size_t)py * w2 + px;      // image pixel (from the window origin)
       f32x4 acc = zero4();
 #pragma unroll
       for (int dy = 0; dy < F3; dy++)
 #pragma unroll
         for (int dx = 0; dx < F3; dx++) {
-          const float dv = d3g[q + d3off - (dy * w2 + dx)];
+          const float dv = d3g[g + d3off - (dy * gw + dx)];
           const f32x4 wv = *reinterpret_cast<const f32x4*>(w3s + (dy * F3 + dx) * N2 + 4 * cq);
 #pragma unroll
           for (int i = 0; i < 4; i++) acc[i] += dv * wv[i];
         }
-      const f32x4 m = *reinterpret_cast<const f32x4*>(a2 + (size_t)q * N2 + 4 * cq);
+      const f32x4 m = *reinterpret_cast<const f32x4*>(a2 + q * N2 + 4 * cq);
 #pragma unroll
       for (int i = 0; i < 4; i++) acc[i] = m[i] > 0.0f ? acc[i] : 0.0f;
-      *reinterpret_cast<f32x4*>(d2 + (size_t)q * N2 + 4 * cq) = acc;
+      *reinterpret_cast<f32x4*>(d2 + q * N2 + 4 * cq) = acc;
     }
-    __syncthreads();
   }
 }
 
@@ -557,51 +632,53 @@ __global__ __launch_bounds__(256) void l3_grad_kernel(const float* __restrict__ 
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* d3g = sm;
   const int lane = lane_id(), wave = wave_id(), lq = lane & 15, lg = lane >> 4;
-  const int npx2 = w2 * h2, d3off = (F3 - 1) * (w2 + 1), nd3 = npx2 + d3off + 4;
-  const int w3 = w2 - F3 + 1, h3 = h2 - F3 + 1;
-  int goff[TT];  // window of tap 16t + lq (rows past K3 read a real window, discarded)
-#pragma unroll
-  for (int t = 0; t < TT; t++) {
-    const int tap = min(16 * t + lq, K3 - 1);
-    goff[t] = d3off - ((tap / F3) * w2 + tap % F3);
-  }
   f32x4 acc[TT][NT];
 #pragma unroll
   for (int t = 0; t < TT; t++)
 #pragma unroll
     for (int u = 0; u < NT; u++) acc[t][u] = zero4();
   float gb = 0.0f;
-  const int ngrp = (npx2 + 3) / 4;
-  for (int s = blockIdx.x; s < batch; s += gridDim.x) {
-    stage_d3<F3>(D3, d3g, s, w2, h2, nd3);
-    const float* a2 = A2 + (size_t)s * npx2 * N2 + lq;
+  const long long items = l1_items(w2, h2, kD3Win, batch);
+  for (long long it = blockIdx.x; it < items; it += gridDim.x) {
+    const L1Win win(it, w2, h2, kD3Win);
+    stage_d3_window<F3>(D3, d3g, win, w2, h2, &gb);
+    const int gw = win.ow + F3 - 1, d3off = (F3 - 1) * (gw + 1);
+    const int npxw = win.ow * win.oh, ngrp = (npxw + 3) / 4;
+    int goff[TT];  // window of tap 16t + lq (rows past K3 read a real window, discarded)
+#pragma unroll
+    for (int t = 0; t < TT; t++) {
+      const int tap = min(16 * t + lq, K3 - 1);
+      goff[t] = d3off - ((tap / F3) * gw + tap % F3);
+    }
+    const float* a2 = A2 + ((size_t)win.s * w2 * h2 + (size_t)win.y0 * w2 + win.x0) * N2 + lq;
     // the A2 operands (HBM) of the wave's next pixel group are in flight
     // while this group's MFMAs run
     float bn[NT];
     auto load_b = [&](int g) {
-      const int qc = min(4 * g + lg, npx2 - 1);
+      const size_t qi = win_px(min(4 * g + lg, npxw - 1), win.ow, w2);
 #pragma unroll
-      for (int u = 0; u < NT; u++) bn[u] = a2[(size_t)qc * N2 + 16 * u];
+      for (int u = 0; u < NT; u++) bn[u] = a2[qi * N2 + 16 * u];
     };
     if (wave < ngrp) load_b(wave);
+    // window pixel q = 4g + lg as (row qy, column qx), advanced by 4 kWaves
+    // pixels per step without a division
+    int qy = (4 * wave + lg) / win.ow, qx = 4 * wave + lg - qy * win.ow;
     for (int g = wave; g < ngrp; g += kWaves) {
       const int q = 4 * g + lg;
-      const bool ok = q < npx2;
-      const int qc = ok ? q : npx2 - 1;
+      const bool ok = q < npxw;
+      const int gq = ok ? qy * gw + qx : 0;  // window grid pixel (rows past the window: unused)
+      for (qx += 4 * kWaves; qx >= win.ow; qx -= win.ow) ++qy;
       float av[TT], bv[NT];
 #pragma unroll
       for (int u = 0; u < NT; u++) bv[u] = bn[u];
       if (g + kWaves < ngrp) load_b(g + kWaves);
 #pragma unroll
-      for (int t = 0; t < TT; t++) av[t] = ok ? d3g[qc + goff[t]] : 0.0f;
+      for (int t = 0; t < TT; t++) av[t] = ok ? d3g[gq + goff[t]] : 0.0f;
 #pragma unroll
       for (int t = 0; t < TT; t++)
 #pragma unroll
         for (int u = 0; u < NT; u++) acc[t][u] = mma16(av[t], bv[u], acc[t][u]);
     }
-    const float* d3 = D3 + (size_t)s * w3 * h3;
-    for (int i = threadIdx.x; i < w3 * h3; i += blockDim.x) gb += d3[i];
-    __syncthreads();
   }
   // block reduction (waves in order) reusing the d3g area
   float* red = sm;
@@ -641,18 +718,6 @@ __global__ __launch_bounds__(256) void l3_grad_kernel(const float* __restrict__ 
 constexpr uint32_t kGridCap = 2048;   // pointwise kernels: 8 blocks per CU
 constexpr uint32_t kSlabCap = 512;    // gradient kernels: slab count (2 blocks per CU)
 
-bool tile_fits(uint32_t w, uint32_t h) { return w <= (uint32_t)kXS && h <= (uint32_t)kXS; }
-
-template <typename K>
-int set_lds(K kernel, size_t bytes) {
-  if (bytes <= 64 * 1024) return SRCNN_OK;
-  hipError_t e = hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     (int)bytes);
-  if (e != hipSuccess)
-    return fail(SRCNN_ERR_HIP, "hipFuncSetAttribute(%zu B): %s", bytes, hipGetErrorString(e));
-  return SRCNN_OK;
-}
-
 // per-block slabs [gW (nW) | gB (nB)] -> gW += rows, gB += rows (fixed order)
 int reduce_rows(const float* slab, int nslab, int nW, int nB, float* gW, float* gB, hipStream_t s) {
   SRCNN_PROFILE("slab_reduce", s);
@@ -668,12 +733,24 @@ int reduce_rows(const float* slab, int nslab, int nW, int nB, float* gW, float* 
 #define SRCNN_N1_SHAPES(X) X(32, 9) X(64, 9) X(128, 9) X(32, 5) X(64, 5) X(64, 3)
 #define SRCNN_N3_SHAPES(X) X(16, 5) X(32, 5) X(64, 5) X(16, 3) X(32, 3) X(64, 3)
 
-size_t l3_fwd_lds(int F3, uint32_t w2, uint32_t h2) { return (size_t)w2 * h2 * F3 * F3 * sizeof(float); }
+// layer-3 forward window: the largest output side wo whose (wo + F3 - 1)^2 Q
+// rows fit the default 64 KiB of LDS (21 at F3 = 5: a 33x33 training tile is
+// one window), and the LDS its (clipped) window needs
+int l3_fwd_wo(int F3) {
+  int wo = 1;
+  while ((size_t)(wo + F3) * (wo + F3) * F3 * F3 * sizeof(float) <= 64 * 1024) ++wo;
+  return wo;
+}
+size_t l3_fwd_lds(int F3, uint32_t w2, uint32_t h2) {
+  const uint32_t side = (uint32_t)(l3_fwd_wo(F3) + F3 - 1);
+  return (size_t)std::min(w2, side) * std::min(h2, side) * F3 * F3 * sizeof(float);
+}
+// delta3 window grid of the delta2 / gW3 kernels
 size_t d3_lds(int F3, uint32_t w2, uint32_t h2) {
-  return ((size_t)w2 * h2 + (F3 - 1) * (w2 + 1) + 4) * sizeof(float);
+  return ((size_t)(std::min<uint32_t>(w2, kD3Win) + F3 - 1) * (std::min<uint32_t>(h2, kD3Win) + F3 - 1)) *
+         sizeof(float);
 }
 constexpr size_t kLdsCap = 64 * 1024;   // the default dynamic LDS of a launch
-constexpr size_t kLdsMax = 160 * 1024;  // with hipFuncSetAttribute (one block per CU)
 
 }  // namespace
 
@@ -696,8 +773,9 @@ int try_conv_fwd(const float* in, float* out, const float* W, const float* B, ui
 #undef SRCNN_PW_F
     return 0;
   }
-  if (n_prev == 1 && tile_fits(in_w, in_h)) {
-    const uint32_t grid = std::min<uint32_t>(batch, 1024);
+  if (n_prev == 1 && in_w >= f && in_h >= f) {
+    const long long items = l1_items((int)(in_w - f + 1), (int)(in_h - f + 1), kXS - (int)f + 1, (int)batch);
+    const uint32_t grid = (uint32_t)std::min<long long>(items, 1024);
 #define SRCNN_L1_F(N1, F1)                                                                      \
     if (n_cur == N1 && f == F1) {                                                               \
       SRCNN_PROFILE("conv_fwd_l1_mfma", s);                                                     \
@@ -710,15 +788,16 @@ int try_conv_fwd(const float* in, float* out, const float* W, const float* B, ui
 #undef SRCNN_L1_F
     return 0;
   }
-  if (n_cur == 1 && l3_fwd_lds(f, in_w, in_h) <= kLdsMax) {
-    const uint32_t grid = std::min<uint32_t>(batch, 1024);
+  if (n_cur == 1) {  // windowed: any image size
+    const int wo = l3_fwd_wo((int)f);
+    const long long items = l1_items((int)(in_w - f + 1), (int)(in_h - f + 1), wo, (int)batch);
+    const uint32_t grid = (uint32_t)std::min<long long>(items, 1024);
     const size_t lds = l3_fwd_lds(f, in_w, in_h);
 #define SRCNN_L3_F(N2, F3)                                                                      \
     if (n_prev == N2 && f == F3) {                                                              \
-      if (int rc = set_lds(l3_fwd_kernel<N2, F3>, lds)) return rc;                              \
       SRCNN_PROFILE("conv_fwd_l3_mfma", s);                                                     \
       hipLaunchKernelGGL((l3_fwd_kernel<N2, F3>), dim3(grid), dim3(256), lds, s, in, W, B, out, \
-                         (int)in_w, (int)in_h, (int)batch, relu);                               \
+                         (int)in_w, (int)in_h, (int)batch, relu, wo);                           \
       SRCNN_LAUNCH_TRY();                                                                       \
       return 1;                                                                                 \
     }
@@ -752,7 +831,7 @@ int try_conv_delta(const float* d_next, const float* y_curr, float* d_curr, cons
   if (n_next == 1) {
     const size_t lds = (size_t)f_next * f_next * n_curr * sizeof(float) + d3_lds(f_next, curr_w, curr_h);
     if (lds > kLdsCap) return 0;
-    const uint32_t grid = std::min<uint32_t>(batch, 2048);
+    const uint32_t grid = (uint32_t)std::min<long long>(l1_items((int)curr_w, (int)curr_h, kD3Win, (int)batch), 2048);
 #define SRCNN_L3_D(N2, F3)                                                                     \
     if (n_curr == N2 && f_next == F3) {                                                        \
       SRCNN_PROFILE("conv_delta_l3", s);                                                       \
@@ -777,7 +856,7 @@ GradKind grad_kind(uint32_t n_prev, uint32_t n_cur, uint32_t f, uint32_t out_w, 
 #undef SRCNN_PW_Q
     return GradKind::None;
   }
-  if (n_prev == 1 && tile_fits(out_w + f - 1, out_h + f - 1)) {
+  if (n_prev == 1) {  // windowed: any image size
 #define SRCNN_L1_Q(N1, F1) if (n_cur == N1 && f == F1) return GradKind::L1;
     SRCNN_N1_SHAPES(SRCNN_L1_Q)
 #undef SRCNN_L1_Q
@@ -790,13 +869,16 @@ GradKind grad_kind(uint32_t n_prev, uint32_t n_cur, uint32_t f, uint32_t out_w, 
   }
   return GradKind::None;
 }
-uint32_t grad_grid(GradKind k, uint32_t out_w, uint32_t out_h, uint32_t batch) {
+uint32_t grad_grid(GradKind k, uint32_t f, uint32_t out_w, uint32_t out_h, uint32_t batch) {
   if (k == GradKind::Pointwise) {
     const long long npx = (long long)batch * out_w * out_h;
     return blocks_for((npx + 7) / 8, 8 * kWaves, kSlabCap);
   }
-  // per-sample kernels: more resident blocks where registers / LDS allow it
-  return std::min<uint32_t>(batch, k == GradKind::L3 ? 4 * kSlabCap : kSlabCap);
+  // per-window kernels: more resident blocks where registers / LDS allow it
+  if (k == GradKind::L1)
+    return (uint32_t)std::min<long long>(l1_items((int)out_w, (int)out_h, kXS - (int)f + 1, (int)batch), kSlabCap);
+  return (uint32_t)std::min<long long>(
+      l1_items((int)(out_w + f - 1), (int)(out_h + f - 1), kD3Win, (int)batch), 4 * kSlabCap);
 }
 }  // namespace
 
@@ -806,7 +888,7 @@ size_t grad_workspace_bytes(uint32_t n_prev, uint32_t n_cur, uint32_t f, uint32_
   const GradKind k = grad_kind(n_prev, n_cur, f, out_w, out_h);
   if (k == GradKind::None) return 0;
   const size_t P = (size_t)f * f * n_prev * n_cur + n_cur;
-  return (size_t)grad_grid(k, out_w, out_h, batch) * P * sizeof(float);
+  return (size_t)grad_grid(k, f, out_w, out_h, batch) * P * sizeof(float);
 }
 
 int try_conv_grad_acc(const float* in, const float* d, float* gW, float* gB, uint32_t n_prev,
@@ -817,7 +899,7 @@ int try_conv_grad_acc(const float* in, const float* d, float* gW, float* gB, uin
     return rc;
   const GradKind k = grad_kind(n_prev, n_cur, f, out_w, out_h);
   if (k == GradKind::None) return 0;
-  const uint32_t grid = grad_grid(k, out_w, out_h, batch);
+  const uint32_t grid = grad_grid(k, f, out_w, out_h, batch);
   const int nW = (int)(f * f * n_prev * n_cur), nB = (int)n_cur;
   const size_t need = (size_t)grid * (nW + nB) * sizeof(float);
   if (ws_bytes < need)

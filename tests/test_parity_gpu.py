@@ -239,7 +239,13 @@ FWD_SHAPES = [
     (32, 16, 1, 25, 25, 3, 1, True),    # example L2
     (16, 1, 5, 25, 25, 3, 0, True),     # example L3
     (64, 32, 1, 7, 5, 1, 0, True),      # pointwise: ragged pixel count, no ReLU
-    (1, 64, 9, 41, 41, 2, 1, False),    # tile past the layer-1 kernel's LDS image
+    (1, 64, 9, 41, 41, 2, 1, True),     # past one 40x40 input window: 2x2 windows
+    (1, 64, 9, 100, 71, 2, 1, True),    # 4x2 windows, ragged right / bottom ones
+    (1, 32, 5, 77, 45, 1, 1, True),     # f1 = 5: 36x36 output windows
+    (1, 128, 9, 128, 128, 1, 1, True),  # the reference's 128 px samples (wide L1)
+    (32, 1, 5, 64, 50, 2, 0, True),     # layer 3 past one 25x25 A2 window, ragged
+    (16, 1, 3, 90, 47, 1, 0, True),     # f3 = 3: 39x39 output windows
+    (32, 1, 5, 120, 120, 1, 0, True),   # A2 of a 128 px sample
     (128, 64, 5, 25, 25, 1, 0, False),  # wide L2 without ReLU: generic
     # the wide net on 25x25 tiles (host spec geometry)
     (1, 128, 9, 25, 25, 3, 1, True),
@@ -281,6 +287,8 @@ DELTA_SHAPES = [
     (32, 1, 3, 9, 6, 2, True),       # f3 = 3, non-square
     (64, 1, 5, 13, 13, 3, True),     # wide net, 25x25 tiles
     (128, 64, 5, 17, 17, 3, True),
+    (32, 1, 5, 140, 70, 1, True),    # delta2 in 64x64 A2 windows, ragged
+    (16, 1, 3, 70, 130, 2, True),
 ]
 
 
@@ -316,6 +324,11 @@ GRAD_SHAPES = [
     (64, 1, 5, 9, 9, 3, True),       # wide net, 25x25 tiles
     (128, 64, 5, 13, 13, 3, True),
     (1, 128, 9, 17, 17, 3, True),
+    (1, 64, 9, 92, 63, 2, True),     # layer 1 in 32x32 output windows, ragged
+    (1, 32, 5, 70, 40, 1, True),     # f1 = 5 windows
+    (1, 64, 9, 120, 120, 1, True),   # a 128 px sample
+    (32, 1, 5, 136, 66, 1, True),    # gW3 in 64x64 A2 windows, ragged
+    (64, 1, 3, 70, 129, 2, True),
 ]
 
 
@@ -348,12 +361,14 @@ NETS = {"default": (64, 32, 9, 1, 5), "wide": (128, 64, 9, 5, 5), "tiny": (8, 4,
 
 def expected_train_path(name, size, path):
     """Kernel family srcnn_train_fwd_bwd must report (srcnn_last_path): the
-    fused f2 == 1 kernels take tiles up to 39x39 (l12's and d1's LDS images);
-    past 33x33 layer 3 runs on the op-level kernels between them."""
-    if path == 1:
+    fused f2 == 1 kernels take tiles up to 39x39 (l12's and d1's LDS images;
+    past 33x33 layer 3 runs on the op-level kernels between them); larger
+    tiles run every conv on the windowed op-level gfx950 kernels ("fast");
+    nets outside the instantiated shapes (tiny: n1 = 8) on the generic ones."""
+    if path == 1 or name == "tiny":
         return {"generic"}
-    if name in ("default", "example", "default_f3") and size <= 39:
-        return {"fused"}
+    if name in ("default", "example", "default_f3"):
+        return {"fused"} if size <= 39 else {"fast"}
     if name == "wide":
         return {"wide"}
     return {"generic", "fast"}
@@ -370,7 +385,11 @@ def expected_train_path(name, size, path):
                                              # train_samples36 (profile.py:7)
                                              ("default", 9, 36), ("example", 5, 39),
                                              ("default", 300, 36), ("default_f3", 7, 33),
-                                             ("default", 3, 40)])
+                                             ("default", 3, 40),
+                                             # past the fused tiles: op-level windowed kernels,
+                                             # e.g. the reference's 128 px samples
+                                             # (generate_training_samples.py -s 128)
+                                             ("default", 2, 128), ("example", 3, 64)])
 def test_train_step_vs_oracle(S, path, name, batch, size):
     cfg = NETS[name]
     net = S.Net(*cfg)
