@@ -209,11 +209,50 @@ constexpr int kImgSlack = 256;                // floats: one DMA instruction pas
 
 struct CGeom {
   int in_w, in_h, pad;    // unpadded input, zero border
-  int img_w, img_h;       // staged image = input + 2 pad
+  int img_w, img_h;       // largest staged image (window output + F - 1 per side)
   int out_w, out_h, npx;  // output
   int batch;
   int xw, xh;             // delta1 + gW1: the X tile (layer-1 input)
+  int wo;                 // > 0: windows of wo x wo outputs (op-level calls on large
+                          // images); 0: the whole image is one window
 };
+
+// Work item `it` = (image s, output window, 64-channel part).  The window's
+// staged image is the padded input over [x0, x0 + iw) x [y0, y0 + ih) (padded
+// coordinates; real = padded - pad, zero outside the input), iw x ih = the
+// largest window's image.
+struct CWin {
+  int s, part, x0, y0, ow, oh, iw, ih;
+};
+template <int F, int NP>
+__device__ __forceinline__ CWin conv_win(int it, const CGeom& g) {
+  CWin w;
+  const int rest = it / NP;
+  w.part = it - rest * NP;
+  if (g.wo == 0) {
+    w.s = rest;
+    w.x0 = w.y0 = 0;
+    w.ow = g.out_w;
+    w.oh = g.out_h;
+  } else {
+    const int nwx = (g.out_w + g.wo - 1) / g.wo, nwin = nwx * ((g.out_h + g.wo - 1) / g.wo);
+    w.s = rest / nwin;
+    const int wi = rest - w.s * nwin, wy = wi / nwx;
+    w.x0 = (wi - wy * nwx) * g.wo;
+    w.y0 = wy * g.wo;
+    w.ow = min(g.wo, g.out_w - w.x0);
+    w.oh = min(g.wo, g.out_h - w.y0);
+  }
+  // every window stages the full img_w x img_h image (the tap offsets are
+  // formed with img_w); an edge window's columns / rows past the input read
+  // the zero source
+  w.iw = g.img_w;
+  w.ih = g.img_h;
+  return w;
+}
+inline int conv_windows(const CGeom& g) {
+  return g.wo == 0 ? 1 : ((g.out_w + g.wo - 1) / g.wo) * ((g.out_h + g.wo - 1) / g.wo);
+}
 
 constexpr int kXBuf = kXTile + 64;  // X tile buffer of the fused gW1 epilogue
 
@@ -246,9 +285,8 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restri
   extern __shared__ float smem[];
   const int lane = lane_id(), wave = wave_id(), j = lane & 31, h = lane >> 5;
   const int nt = wave & 1, mg = wave >> 1;
-  const int img_px = g.img_w * g.img_h, slots = img_px * 5, kdma = (slots + 63) / 64;
-  const int buf_floats = img_px * kPS + kImgSlack;
-  const int nitems = g.batch * NP;
+  const int buf_floats = g.img_w * g.img_h * kPS + kImgSlack;  // the largest window image
+  const int nitems = g.batch * NP * (g.wo == 0 ? 1 : ((g.out_w + g.wo - 1) / g.wo) * ((g.out_h + g.wo - 1) / g.wo));
   float* const xsm = smem + 2 * buf_floats;  // G1: 2 X tile buffers (item parity)
   int toffx[TT];
   float fill[TT];
@@ -262,7 +300,8 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restri
     toffx[tt] = G1 ? (tc / F1) * kXS + tc % F1 : 0;
     gacc[tt] = zero16();
   }
-  // X tile of item it -> xsm[parity] by 4-byte LDS-DMA (stride kXS, zero fill)
+  // X tile of item it -> xsm[parity] by 4-byte LDS-DMA (stride kXS, zero fill;
+  // G1 runs single-window only, so the item's image is it / NP)
   auto xdma = [&](int it, int par) {
     const int s = it / NP;
     float* dst = xsm + par * kXBuf;
@@ -277,35 +316,40 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restri
   // tile m (dy outside [dlo, dhi]) is skipped for that tile (wave-uniform
   // branches around MFMA groups that hold no memory operations)
   int dlo[MT], dhi[MT];
-#pragma unroll
-  for (int m = 0; m < MT; m++) {
-    const int o = min(32 * (2 * m + mg) + j, g.npx - 1), oy = o / g.out_w;
-    abase[m] = (oy * g.img_w + o - oy * g.out_w) * kPS + 4 * h;
-    const int pa = min(32 * (2 * m + mg), g.npx - 1), pb = min(pa + 31, g.npx - 1);
-    dlo[m] = __builtin_amdgcn_readfirstlane(g.pad - pb / g.out_w);
-    dhi[m] = __builtin_amdgcn_readfirstlane(g.pad + g.in_h - 1 - pa / g.out_w);
-  }
-  // one LDS-DMA instruction k (64 slots of 16 B) of chunk c of item it
-  auto dma = [&](int it, int c, float* buf, int k) {
-    const int s = it / NP;
+  // one LDS-DMA instruction k (64 slots of 16 B) of chunk c of window wn
+  auto dma = [&](const CWin& wn, int c, float* buf, int k) {
     const int slot = k * 64 + lane;
     const int pix = slot / 5, q = slot - 5 * pix;
-    const int iy = pix / g.img_w, ix = pix - iy * g.img_w;
-    const int y = iy - g.pad, x = ix - g.pad;
-    const bool ok = q < 4 && slot < slots && y >= 0 && y < g.in_h && x >= 0 && x < g.in_w;
+    const int iy = pix / wn.iw, ix = pix - iy * wn.iw;
+    const int y = wn.y0 + iy - g.pad, x = wn.x0 + ix - g.pad;
+    const bool ok = q < 4 && slot < wn.iw * wn.ih * 5 && y >= 0 && y < g.in_h && x >= 0 && x < g.in_w;
     const float* src =
-        ok ? in + ((size_t)(s * g.in_h + y) * g.in_w + x) * CIN + c * kCC + 4 * q : g_zero_src;
+        ok ? in + ((size_t)(wn.s * g.in_h + y) * g.in_w + x) * CIN + c * kCC + 4 * q : g_zero_src;
     dma16(src, buf + k * 256);
   };
+  auto kdma_of = [](const CWin& wn) { return (wn.iw * wn.ih * 5 + 63) / 64; };
   float* const buf0 = smem;
   float* const buf1 = smem + buf_floats;
-  if ((int)blockIdx.x < nitems)
-    for (int k = wave; k < kdma; k += 4) dma(blockIdx.x, 0, buf0, k);
+  if ((int)blockIdx.x < nitems) {
+    const CWin w0 = conv_win<F, NP>(blockIdx.x, g);
+    for (int k = wave; k < kdma_of(w0); k += 4) dma(w0, 0, buf0, k);
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   int bsel = 0, ipar = 0;
   for (int it = blockIdx.x; it < nitems; it += gridDim.x, ipar ^= 1) {
-    const int s = it / NP, part = it - s * NP;
+    const CWin cw = conv_win<F, NP>(it, g);
+    const int s = cw.s, part = cw.part, npxw = cw.ow * cw.oh;
+    // the next item's window (its first chunk is staged under this item's last)
+    const CWin wnext = conv_win<F, NP>(min(it + (int)gridDim.x, nitems - 1), g);
+#pragma unroll
+    for (int m = 0; m < MT; m++) {
+      const int o = min(32 * (2 * m + mg) + j, npxw - 1), oy = o / cw.ow;
+      abase[m] = (oy * cw.iw + o - oy * cw.ow) * kPS + 4 * h;
+      const int pa = min(32 * (2 * m + mg), npxw - 1), pb = min(pa + 31, npxw - 1);
+      dlo[m] = __builtin_amdgcn_readfirstlane(g.pad - (cw.y0 + pb / cw.ow));
+      dhi[m] = __builtin_amdgcn_readfirstlane(g.pad + g.in_h - 1 - (cw.y0 + pa / cw.ow));
+    }
     if constexpr (G1) xdma(it, ipar);  // lands before the first chunk barrier
     const float4* wp = reinterpret_cast<const float4*>(Wimg) + (size_t)(part * 2 + nt) * KS * 64 + lane;
     f32x16 acc[MT];
@@ -329,6 +373,8 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restri
         nc = 0;
       }
       const bool stage = nit < nitems;
+      const CWin& wd = nc == 0 ? wnext : cw;  // the window the staged chunk belongs to
+      const int kdma = kdma_of(wd);
       float4 a[MT], an[MT];
 #pragma unroll
       for (int m = 0; m < MT; m++) a[m] = *reinterpret_cast<const float4*>(cur + abase[m]);
@@ -349,7 +395,7 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restri
 #pragma unroll
           for (int q = 0; q < 2; q++) {
             const int k = wave + 4 * (2 * t + q);
-            if (stage && k < kdma && !(kWDiag & 4)) dma(nit, nc, nxt, k);
+            if (stage && k < kdma && !(kWDiag & 4)) dma(wd, nc, nxt, k);
           }
           // k-step (t, 0) while (t, 1) loads; k-step (t, 1) while (t + 1, 0)
           // loads.  sched_barriers pin the order: left alone, the scheduler
@@ -383,7 +429,8 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restri
       bsel ^= 1;
     }
     const int n = part * 64 + nt * 32 + j;
-    const size_t obase = (size_t)s * g.npx * COUT + n;
+    // output pixels of the window, from its origin (G1: one window per image)
+    const size_t obase = ((size_t)s * g.npx + (size_t)cw.y0 * g.out_w + cw.x0) * COUT + n;
     if constexpr (G1) {
       // delta1 = relu'(A1) * acc (mask loads one tile ahead), then
       // gW1 += Xwin^T delta1 on the matrix core
@@ -439,8 +486,9 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restri
 #pragma unroll
         for (int r = 0; r < 16; r++) {
           const int pix = p0 + crow(r, 0);
-          if (pix < g.npx) {
-            const size_t idx = obase + (size_t)pix * COUT;
+          if (pix < npxw) {
+            const int py = cw.ow == g.out_w ? 0 : pix / cw.ow;  // window pixel -> image pixel
+            const size_t idx = obase + (size_t)(pix + py * (g.out_w - cw.ow)) * COUT;
             if (DELTA)
               out[idx] = ycur[idx] > 0.0f ? acc[m][r] : 0.0f;
             else
@@ -788,9 +836,9 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   if (g.w > kXS || g.h > kXS || g.w3 <= 0 || g.h3 <= 0) return 0;
   const int npx1 = g.w1 * g.h1, npx2 = g.w2 * g.h2;
   // L2 forward / delta1 geometry limits (register tiles, LDS images)
-  CGeom cf{g.w1, g.h1, 0, g.w1, g.h1, g.w2, g.h2, npx2, g.batch, 0, 0};
+  CGeom cf{g.w1, g.h1, 0, g.w1, g.h1, g.w2, g.h2, npx2, g.batch, 0, 0, 0};
   CGeom cd{g.w2, g.h2, F2 - 1, g.w2 + 2 * (F2 - 1), g.h2 + 2 * (F2 - 1), g.w1, g.h1, npx1, g.batch,
-           g.w, g.h};
+           g.w, g.h, 0};
   if ((npx2 + 31) / 32 > 2 * NetT::MT2 || (npx1 + 31) / 32 > 2 * NetT::MT4) return 0;
   if (cf.img_w * cf.img_h > kImgMax || cd.img_w * cd.img_h > kImgMax) return 0;
   // wgrad2 bands
@@ -935,15 +983,21 @@ int op_conv_fwd(const float* in, float* out, const float* W, const float* B, uin
                 uint32_t batch, hipStream_t s) {
   if (n_prev != kWN1 || n_cur != kWN2 || f != kWF || !relu) return 0;
   const int ow = (int)in_w - kWF + 1, oh = (int)in_h - kWF + 1;
-  CGeom cf{(int)in_w, (int)in_h, 0, (int)in_w, (int)in_h, ow, oh, ow * oh, (int)batch, 0, 0};
-  if ((cf.npx + 31) / 32 > 2 * WideNet::MT2 || cf.img_w * cf.img_h > kImgMax) return 0;
+  CGeom cf{(int)in_w, (int)in_h, 0, (int)in_w, (int)in_h, ow, oh, ow * oh, (int)batch, 0, 0, 0};
+  if ((cf.npx + 31) / 32 > 2 * WideNet::MT2 || cf.img_w * cf.img_h > kImgMax) {
+    // larger images: 21x21 output windows (441 pixels of the 448 the register
+    // tiles hold; 25x25 = 625 staged pixels)
+    cf.wo = 21;
+    cf.img_w = std::min(ow, cf.wo) + kWF - 1;
+    cf.img_h = std::min(oh, cf.wo) + kWF - 1;
+  }
   float* img = nullptr;
   if (int rc = prepacked_w2(W, &img, s)) return rc;
   const size_t lds = 2 * ((size_t)cf.img_w * cf.img_h * kPS + kImgSlack) * sizeof(float);
   if (int rc = set_lds(conv_mfma_kernel<kWN1, kWN2, kWF, WideNet::MT2, false, 0>, lds)) return rc;
   {
     SRCNN_PROFILE("conv_fwd_wide_mfma", s);
-    const int items = (int)batch * (kWN2 / 64);
+    const int items = (int)batch * (kWN2 / 64) * conv_windows(cf);
     hipLaunchKernelGGL((conv_mfma_kernel<kWN1, kWN2, kWF, WideNet::MT2, false, 0>),
                        dim3(std::min(items, 256)), dim3(256), lds, s, in, img, B,
                        (const float*)nullptr, out, (const float*)nullptr, (float*)nullptr, cf);
@@ -958,15 +1012,21 @@ int op_conv_delta(const float* d_next, const float* y_curr, float* d_curr, const
   if (n_curr != kWN1 || n_next != kWN2 || f_next != kWF) return 0;
   const int nw = (int)curr_w - kWF + 1, nh = (int)curr_h - kWF + 1;
   CGeom cd{nw, nh, kWF - 1, nw + 2 * (kWF - 1), nh + 2 * (kWF - 1), (int)curr_w, (int)curr_h,
-           (int)(curr_w * curr_h), (int)batch, 0, 0};
-  if ((cd.npx + 31) / 32 > 2 * WideNet::MT4 || cd.img_w * cd.img_h > kImgMax) return 0;
+           (int)(curr_w * curr_h), (int)batch, 0, 0, 0};
+  if ((cd.npx + 31) / 32 > 2 * WideNet::MT4 || cd.img_w * cd.img_h > kImgMax) {
+    // larger images: 25x25 output windows (625 of the 640 pixels the register
+    // tiles hold; 29x29 = 841 staged pixels)
+    cd.wo = 25;
+    cd.img_w = std::min((int)curr_w, cd.wo) + kWF - 1;
+    cd.img_h = std::min((int)curr_h, cd.wo) + kWF - 1;
+  }
   float* img = nullptr;
   if (int rc = prepacked_w2(W_next, &img, s)) return rc;
   const size_t lds = 2 * ((size_t)cd.img_w * cd.img_h * kPS + kImgSlack) * sizeof(float);
   if (int rc = set_lds(conv_mfma_kernel<kWN2, kWN1, kWF, WideNet::MT4, true, 0>, lds)) return rc;
   {
     SRCNN_PROFILE("conv_delta_wide_mfma", s);
-    const int items = (int)batch * (kWN1 / 64);
+    const int items = (int)batch * (kWN1 / 64) * conv_windows(cd);
     hipLaunchKernelGGL((conv_mfma_kernel<kWN2, kWN1, kWF, WideNet::MT4, true, 0>),
                        dim3(std::min(items, 256)), dim3(256), lds, s, d_next,
                        img + align_f(WideNet::W2), (const float*)nullptr, y_curr, d_curr,

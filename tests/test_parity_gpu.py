@@ -246,6 +246,7 @@ FWD_SHAPES = [
     (32, 1, 5, 64, 50, 2, 0, True),     # layer 3 past one 25x25 A2 window, ragged
     (16, 1, 3, 90, 47, 1, 0, True),     # f3 = 3: 39x39 output windows
     (32, 1, 5, 120, 120, 1, 0, True),   # A2 of a 128 px sample
+    (128, 64, 5, 60, 45, 1, 1, True),   # wide L2 in 21x21 output windows, ragged
     (128, 64, 5, 25, 25, 1, 0, False),  # wide L2 without ReLU: generic
     # the wide net on 25x25 tiles (host spec geometry)
     (1, 128, 9, 25, 25, 3, 1, True),
@@ -288,6 +289,7 @@ DELTA_SHAPES = [
     (64, 1, 5, 13, 13, 3, True),     # wide net, 25x25 tiles
     (128, 64, 5, 17, 17, 3, True),
     (32, 1, 5, 140, 70, 1, True),    # delta2 in 64x64 A2 windows, ragged
+    (128, 64, 5, 61, 40, 1, True),   # wide delta1 in 25x25 windows
     (16, 1, 3, 70, 130, 2, True),
 ]
 
