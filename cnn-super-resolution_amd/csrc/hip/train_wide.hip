@@ -707,8 +707,11 @@ constexpr int kGBuf = kGAFl + (kBandPx + 4) * kGDS + 256;
 
 struct G2Geom {
   int w1, h1, w2, h2;
-  int rows, nbands;  // output rows per band, bands per sample
+  int rows, nbands;  // output rows per band, bands per sample (nbx * band rows)
   int batch, groups;
+  int cols, nbx;     // output columns per band (w2: full rows), bands per band row
+  int aw;            // A1 band image width cols + F - 1 (a kernel argument, so the
+                     // tap offsets stay scalar: 4 adds per k-step, not 7)
 };
 
 template <int CIN, int COUT, int F>
@@ -727,12 +730,15 @@ __global__ __launch_bounds__(512, 1) void wgrad2_kernel(const float* __restrict_
 #pragma unroll
   for (int t = 0; t < FF; t++) acc[t] = zero4();
   float gb = 0.0f;
+  // a band is rows x cols output pixels (row-major, cols = w2 for full-width
+  // bands); its A1 image is (rows + F - 1) x aw pixels, aw = cols + F - 1
+  const int aw = g.aw;
   int abase[16];
-  const int bandpx_full = g.rows * g.w2;
+  const int bandpx_full = g.rows * g.cols;
 #pragma unroll
   for (int kq = 0; kq < 16; kq++) {
-    const int k = min(4 * kq + gq, bandpx_full - 1), ky = k / g.w2, kx = k - ky * g.w2;
-    abase[kq] = (ky * g.w1 + kx) * kGAS + 16 * ct + i;
+    const int k = min(4 * kq + gq, bandpx_full - 1), ky = k / g.cols, kx = k - ky * g.cols;
+    abase[kq] = (ky * aw + kx) * kGAS + 16 * ct + i;
   }
   const int dlane = kGAFl + gq * kGDS + 16 * nt + i;
   for (int e = threadIdx.x; e < 2 * kGBuf; e += 512) smem[e] = 0.0f;
@@ -741,21 +747,40 @@ __global__ __launch_bounds__(512, 1) void wgrad2_kernel(const float* __restrict_
   const int nsamp = g.batch > grp ? (g.batch - grp + g.groups - 1) / g.groups : 0;
   const int nunits = nsamp * g.nbands;
   auto stage = [&](int u, float* buf) {
-    const int s = grp + (u / g.nbands) * g.groups, b = u % g.nbands;
-    const int y0 = b * g.rows, rb = min(g.rows, g.h2 - y0);
-    const int apx = (rb + F - 1) * g.w1, aslots = apx * 12;
-    const float* asrc = A1 + ((size_t)s * g.h1 * g.w1 + (size_t)y0 * g.w1) * CIN + 32 * cq;
-    for (int k = wave; k * 64 < aslots; k += 8) {
-      const int slot = k * 64 + lane, pix = slot / 12, q = slot - 12 * pix;
-      const bool ok = q < 8 && slot < aslots;
-      dma16(ok ? asrc + (size_t)pix * CIN + 4 * q : g_zero_src, buf + k * 256);
-    }
-    const int dpx = rb * g.w2, dslots = (kBandPx + 4) * 20;
-    const float* dsrc = D2 + ((size_t)s * g.h2 * g.w2 + (size_t)y0 * g.w2) * COUT;
-    for (int k = wave; k * 64 < dslots; k += 8) {
-      const int slot = k * 64 + lane, pix = slot / 20, q = slot - 20 * pix;
-      const bool ok = q < 16 && pix < dpx;
-      dma16(ok ? dsrc + (size_t)pix * COUT + 4 * q : g_zero_src, buf + kGAFl + k * 256);
+    const int s = grp + (u / g.nbands) * g.groups, b = u % g.nbands, by = b / g.nbx;
+    const int y0 = by * g.rows, rb = min(g.rows, g.h2 - y0);
+    const int x0 = (b - by * g.nbx) * g.cols, cb = min(g.cols, g.w2 - x0);
+    // A1 window rows y0 .. y0 + rb + F - 2, columns x0 .. x0 + aw - 1 (past the
+    // image: zero)
+    const int aslots = (rb + F - 1) * aw * 12;
+    const float* asrc = A1 + ((size_t)s * g.h1 * g.w1 + (size_t)y0 * g.w1 + x0) * CIN + 32 * cq;
+    const int dslots = (kBandPx + 4) * 20;
+    const float* dsrc = D2 + ((size_t)s * g.h2 * g.w2 + (size_t)y0 * g.w2 + x0) * COUT;
+    if (g.nbx == 1) {  // full-width bands: the band's rows are contiguous in HBM
+      for (int k = wave; k * 64 < aslots; k += 8) {
+        const int slot = k * 64 + lane, pix = slot / 12, q = slot - 12 * pix;
+        const bool ok = q < 8 && slot < aslots;
+        dma16(ok ? asrc + (size_t)pix * CIN + 4 * q : g_zero_src, buf + k * 256);
+      }
+      const int dpx = rb * g.w2;
+      for (int k = wave; k * 64 < dslots; k += 8) {
+        const int slot = k * 64 + lane, pix = slot / 20, q = slot - 20 * pix;
+        const bool ok = q < 16 && pix < dpx;
+        dma16(ok ? dsrc + (size_t)pix * COUT + 4 * q : g_zero_src, buf + kGAFl + k * 256);
+      }
+    } else {
+      for (int k = wave; k * 64 < aslots; k += 8) {
+        const int slot = k * 64 + lane, pix = slot / 12, q = slot - 12 * pix;
+        const int py = pix / aw, px = pix - py * aw;
+        const bool ok = q < 8 && slot < aslots && x0 + px < g.w1;
+        dma16(ok ? asrc + ((size_t)py * g.w1 + px) * CIN + 4 * q : g_zero_src, buf + k * 256);
+      }
+      for (int k = wave; k * 64 < dslots; k += 8) {
+        const int slot = k * 64 + lane, pix = slot / 20, q = slot - 20 * pix;
+        const int py = pix / g.cols, px = pix - py * g.cols;
+        const bool ok = q < 16 && py < rb && px < cb;
+        dma16(ok ? dsrc + ((size_t)py * g.w2 + px) * COUT + 4 * q : g_zero_src, buf + kGAFl + k * 256);
+      }
     }
   };
   int bsel = 0;
@@ -771,7 +796,7 @@ __global__ __launch_bounds__(512, 1) void wgrad2_kernel(const float* __restrict_
       if (gbw) gb += b;
 #pragma unroll
       for (int t = 0; t < FF; t++) {
-        const float a = cur[abase[kq] + ((t / F) * g.w1 + t % F) * kGAS];
+        const float a = cur[abase[kq] + ((t / F) * aw + t % F) * kGAS];
         acc[t] = mma16(a, b, acc[t]);
       }
     }
@@ -849,6 +874,9 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   g2.h2 = g.h2;
   g2.rows = std::min(8, kBandPx / g.w2);
   if (g2.rows < 1 || (g2.rows + F2 - 1) * g.w1 > kGAPx) return 0;
+  g2.cols = g.w2;  // full-width bands
+  g2.nbx = 1;
+  g2.aw = g.w1;
   g2.nbands = (g.h2 + g2.rows - 1) / g2.rows;
   g2.batch = g.batch;
   g2.groups = (int)std::min<uint32_t>(batch, 64);
@@ -1042,9 +1070,17 @@ bool g2_geom(uint32_t out_w, uint32_t out_h, uint32_t batch, G2Geom* g2) {
   g2->h2 = (int)out_h;
   g2->w1 = g2->w2 + kWF - 1;
   g2->h1 = g2->h2 + kWF - 1;
+  // full-width bands where a few whole rows fit the band images, else
+  // 16-column x 4-row windows (A1 image 20 x 8 = 160 pixels)
+  g2->cols = g2->w2;
   g2->rows = std::min(8, kBandPx / std::max(1, g2->w2));
-  if (g2->rows < 1 || (g2->rows + kWF - 1) * g2->w1 > kGAPx) return false;
-  g2->nbands = (g2->h2 + g2->rows - 1) / g2->rows;
+  if (g2->rows < 1 || (g2->rows + kWF - 1) * g2->w1 > kGAPx) {
+    g2->cols = 16;
+    g2->rows = kBandPx / 16;
+  }
+  g2->nbx = (g2->w2 + g2->cols - 1) / g2->cols;
+  g2->aw = g2->cols + kWF - 1;
+  g2->nbands = g2->nbx * ((g2->h2 + g2->rows - 1) / g2->rows);
   g2->batch = (int)batch;
   g2->groups = (int)std::min<uint32_t>(batch, 64);
   return true;

@@ -331,6 +331,7 @@ GRAD_SHAPES = [
     (1, 64, 9, 120, 120, 1, True),   # a 128 px sample
     (32, 1, 5, 136, 66, 1, True),    # gW3 in 64x64 A2 windows, ragged
     (64, 1, 3, 70, 129, 2, True),
+    (128, 64, 5, 50, 37, 1, True),   # wide gW2 in 16 x 4 output windows
 ]
 
 
@@ -372,7 +373,7 @@ def expected_train_path(name, size, path):
     if name in ("default", "example", "default_f3"):
         return {"fused"} if size <= 39 else {"fast"}
     if name == "wide":
-        return {"wide"}
+        return {"wide"} if size <= 40 else {"fast"}
     return {"generic", "fast"}
 
 
@@ -391,7 +392,8 @@ def expected_train_path(name, size, path):
                                              # past the fused tiles: op-level windowed kernels,
                                              # e.g. the reference's 128 px samples
                                              # (generate_training_samples.py -s 128)
-                                             ("default", 2, 128), ("example", 3, 64)])
+                                             ("default", 2, 128), ("example", 3, 64),
+                                             ("wide", 2, 48)])
 def test_train_step_vs_oracle(S, path, name, batch, size):
     cfg = NETS[name]
     net = S.Net(*cfg)
