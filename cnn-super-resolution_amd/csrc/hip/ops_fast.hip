@@ -22,7 +22,9 @@
 //
 //   single input channel (n_prev == 1: layer 1, f1 x f1 x 1 -> n1), per
 //   sample with the input tile in LDS:
-//     l1_fwd_kernel     M = pixels (32), N = 32 channels, K = taps (paired)
+//     l1_fwd_kernel     transposed: M = 32 channels, N = pixels (32), K = taps
+//                       (paired), so a lane ends with 4 runs of 4 consecutive
+//                       channels of one pixel: 16-B stores
 //     l1_grad_kernel    gW1 (+ gB1 through a ones row): M = taps, N = n1, K = px
 //
 //   the wide middle layer (5x5, n1 = 128 <-> n2 = 64): train_wide.hip's
@@ -303,13 +305,17 @@ __global__ __launch_bounds__(256) void l1_fwd_kernel(const float* __restrict__ X
   const int lane = lane_id(), wave = wave_id(), j = lane & 31, hh = lane >> 5;
   const int nt = wave % NTW, mg = wave / NTW;
   const int n = 32 * nt + j;
+  // A operand (transposed GEMM): W1[tap kp + KP hh][channel n]
   float wb[KP];
 #pragma unroll
   for (int kp = 0; kp < KP; kp++) {
     const int t = kp + KP * hh;
     wb[kp] = t < K1 ? W1[t * N1 + n] : 0.0f;
   }
-  const float bias = B1[n];
+  // C register 4g + i of lane (j, hh) is channel 32 nt + 8g + 4hh + i of pixel j
+  f32x4 bias[4];
+#pragma unroll
+  for (int g = 0; g < 4; g++) bias[g] = *reinterpret_cast<const f32x4*>(B1 + 32 * nt + 8 * g + 4 * hh);
   for (int i = threadIdx.x; i < kXTile; i += 256) xs[i] = 0.0f;
   const int w1 = w - F1 + 1, h1 = h - F1 + 1;
   constexpr int WO = kXS - F1 + 1;
@@ -322,7 +328,7 @@ __global__ __launch_bounds__(256) void l1_fwd_kernel(const float* __restrict__ X
     __syncthreads();
     stage_x_window<F1>(X, xs, win, w, h);
     __syncthreads();
-    float* dst = A1 + ((size_t)win.s * w1 * h1 + (size_t)win.y0 * w1 + win.x0) * N1 + n;
+    float* dst = A1 + ((size_t)win.s * w1 * h1 + (size_t)win.y0 * w1 + win.x0) * N1 + 32 * nt + 4 * hh;
     for (int m = 2 * mg; m < mtiles; m += 2 * MG) {
       int base[2];
 #pragma unroll
@@ -335,25 +341,26 @@ __global__ __launch_bounds__(256) void l1_fwd_kernel(const float* __restrict__ X
       for (int kp = 0; kp < KP; kp++) {
         const int toff = (kp / F1) * kXS + kp % F1;
         const int dd = (kp % F1 + R < F1) ? dA : dB;
-        acc0 = mma(xs[base[0] + dd + toff], wb[kp], acc0);
-        acc1 = mma(xs[base[1] + dd + toff], wb[kp], acc1);
+        acc0 = mma(wb[kp], xs[base[0] + dd + toff], acc0);
+        acc1 = mma(wb[kp], xs[base[1] + dd + toff], acc1);
       }
-      if (win.ow == w1) {  // the window spans the image rows: pixel offsets as they are
+      // this lane's pixels of the two tiles, as offsets in the image
+      const int p0 = 32 * m + j, p1 = p0 + 32;
+      const size_t q0 = (size_t)win_px(p0, win.ow, w1) * N1, q1 = (size_t)win_px(p1, win.ow, w1) * N1;
 #pragma unroll
-        for (int r = 0; r < 16; r++) {
-          const int p0 = 32 * m + crow(r, hh), p1 = p0 + 32;
-          const float v0 = acc0[r] + bias, v1 = acc1[r] + bias;
-          if (p0 < npx) dst[(size_t)p0 * N1] = relu ? fmaxf(v0, 0.0f) : v0;
-          if (p1 < npx) dst[(size_t)p1 * N1] = relu ? fmaxf(v1, 0.0f) : v1;
-        }
-      } else {
+      for (int g = 0; g < 4; g++) {
+        f32x4 v0, v1;
 #pragma unroll
-        for (int r = 0; r < 16; r++) {
-          const int p0 = 32 * m + crow(r, hh), p1 = p0 + 32;
-          const float v0 = acc0[r] + bias, v1 = acc1[r] + bias;
-          if (p0 < npx) dst[(size_t)win_px(p0, win.ow, w1) * N1] = relu ? fmaxf(v0, 0.0f) : v0;
-          if (p1 < npx) dst[(size_t)win_px(p1, win.ow, w1) * N1] = relu ? fmaxf(v1, 0.0f) : v1;
+        for (int i = 0; i < 4; i++) {
+          v0[i] = acc0[4 * g + i] + bias[g][i];
+          v1[i] = acc1[4 * g + i] + bias[g][i];
+          if (relu) {
+            v0[i] = fmaxf(v0[i], 0.0f);
+            v1[i] = fmaxf(v1[i], 0.0f);
+          }
         }
+        if (p0 < npx) *reinterpret_cast<f32x4*>(dst + q0 + 8 * g) = v0;
+        if (p1 < npx) *reinterpret_cast<f32x4*>(dst + q1 + 8 * g) = v1;
       }
     }
   }
