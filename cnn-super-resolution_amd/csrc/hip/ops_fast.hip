@@ -21,29 +21,32 @@
 //   pixel and no LDS round trip is needed.
 //
 //   single input channel (n_prev == 1: layer 1, f1 x f1 x 1 -> n1), per
-//   sample with the input tile in LDS:
+//   image window (up to (40 - f1 + 1)^2 outputs) with its 40 x 40 input
+//   window in LDS, so any image size runs here:
 //     l1_fwd_kernel     transposed: M = 32 channels, N = pixels (32), K = taps
 //                       (paired), so a lane ends with 4 runs of 4 consecutive
 //                       channels of one pixel: 16-B stores
 //     l1_grad_kernel    gW1 (+ gB1 through a ones row): M = taps, N = n1, K = px
 //
 //   the wide middle layer (5x5, n1 = 128 <-> n2 = 64): train_wide.hip's
-//   conv_mfma (forward, delta1) and wgrad2 kernels (wide::op_*)
+//   conv_mfma (forward, delta1) and wgrad2 kernels (wide::op_*), on image
+//   windows past 31 x 31
 //
 //   single output channel (n_cur == 1 / n_next == 1: layer 3, f3 x f3 x n2
-//   -> 1), per sample:
+//   -> 1), per image window (forward: 21 x 21 outputs; delta2 / gW3: 64 x 64
+//   A2 pixels):
 //     l3_fwd_kernel     Q[q][tap] = A2[q][:] . W3[tap][:] (MFMA, HBM operands),
 //                       A3[p] = B3 + sum_tap Q[p + off(tap)][tap] (LDS)
 //     l3_delta_kernel   delta2[q][c] = relu'(A2) sum_tap delta3(q - off(tap)) W3[tap][c]
-//                       (delta3 on the A2 grid with a zero border, LDS)
+//                       (the window's delta3 neighbourhood with a zero border, LDS)
 //     l3_grad_kernel    gW3[tap][c] = sum_q delta3(q - off(tap)) A2[q][c]: M = taps,
 //                       N = n2, K = A2 pixels
 //
 // Gradients are summed deterministically: per-block slabs, then the
 // fixed-order slab reduction of train_fused.hip adds them into gW / gB (the
 // racy += of backpropagate.cl:110 is not reproduced).  Shapes outside these
-// families (or tiles too large for the per-sample LDS images) return 0 and
-// abi.cpp runs ops_generic.hip instead; srcnn_last_path() reports which.
+// families return 0 and abi.cpp runs ops_generic.hip instead;
+// srcnn_last_path() reports which.
 #include <algorithm>
 
 #include "common.hpp"
