@@ -714,6 +714,13 @@ struct G2Geom {
                      // tap offsets stay scalar: 4 adds per k-step, not 7)
 };
 
+// diagnostics builds only (results invalid): 1 drop the MFMAs, 2 drop the
+// staging DMA after the first band, 4 drop the band barrier
+#ifdef SRCNN_WG2_DIAG
+constexpr int kWg2Diag = SRCNN_WG2_DIAG;
+#else
+constexpr int kWg2Diag = 0;
+#endif
 template <int CIN, int COUT, int F>
 __global__ __launch_bounds__(512, 1) void wgrad2_kernel(const float* __restrict__ A1,
                                                        const float* __restrict__ D2,
@@ -787,9 +794,9 @@ __global__ __launch_bounds__(512, 1) void wgrad2_kernel(const float* __restrict_
   if (nunits > 0) stage(0, smem);
   for (int u = 0; u < nunits; u++) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();  // unit u landed; everyone is done with the other buffer
+    if (!(kWg2Diag & 4) || u == 0) __syncthreads();  // unit u landed; everyone is done with the other buffer
     const float* cur = smem + (bsel ? kGBuf : 0);
-    if (u + 1 < nunits) stage(u + 1, smem + (bsel ? 0 : kGBuf));
+    if (u + 1 < nunits && !(kWg2Diag & 2)) stage(u + 1, smem + (bsel ? 0 : kGBuf));
 #pragma unroll
     for (int kq = 0; kq < 16; kq++) {
       const float b = cur[dlane + kq * 4 * kGDS];
@@ -797,7 +804,8 @@ __global__ __launch_bounds__(512, 1) void wgrad2_kernel(const float* __restrict_
 #pragma unroll
       for (int t = 0; t < FF; t++) {
         const float a = cur[abase[kq] + ((t / F) * aw + t % F) * kGAS];
-        acc[t] = mma16(a, b, acc[t]);
+        if (kWg2Diag & 1) acc[t][0] += a * b;
+        else acc[t] = mma16(a, b, acc[t]);
       }
     }
     bsel ^= 1;
