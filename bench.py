@@ -280,7 +280,7 @@ def cpu_forward_baseline(net, strip_rows=256, reps=3):
     return out
 
 
-def forward_4k(S, net_t, frames=5, warmup=2, w=3840, h=2160):
+def forward_4k(S, net_t, frames=20, warmup=3, w=3840, h=2160):
     """BASELINE.json configs[4]: forward-only inference of one 3840x2160 luma
     frame (fused path), reported as input Mpix/s.  Time with events on the
     stream the kernels run on; per-kernel split from srcnn_profile_*."""
@@ -435,6 +435,7 @@ def wide_training(S, steps=5, warmup=2, batch=4096):
         step()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    _mark("wide timed steps done")
     S.profile_enable(False)
     stats = S.profile_stats()
     work = layer_work(net_t, w, h)
@@ -455,6 +456,14 @@ def wide_training(S, steps=5, warmup=2, batch=4096):
             "tflops": round(flops / (ms * 1e-3) / 1e12, 2),
             "step_roofline": {"t_roof_ms": round(t_roof * 1e3, 4), "frac": round(t_roof * 1e3 / ms, 4)},
             "kernel_path": S.last_path(), "kernels": kernels, "rooflines": rooflines}
+
+
+_T0 = time.perf_counter()
+
+
+def _mark(what):
+    if os.environ.get("SRCNN_BENCH_TRACE"):
+        print("[bench %.1f ms] %s" % ((time.perf_counter() - _T0) * 1e3, what), file=sys.stderr, flush=True)
 
 
 def main():
@@ -537,9 +546,32 @@ def main():
         lambda nb: S.update_all(net, params, grads, mom, 0.9, 1e-3, lr, nb, stream),
         global_tiles, allreduce=comm)
 
-    for _ in range(args.warmup):
-        step()
+    # The single-GPU side lines (the wide net, one 256x256 tile, 4K inference)
+    # are measured before the headline.  Order and pause matter on this part
+    # (tools/debug/first_step.py): right after ~0.15 s of the
+    # wide net's full-power load the GPU stalls the next launch for 8-24 ms
+    # (a power-state transition; a 0.2 s idle pause avoids it), and a step
+    # launched on an idle GPU runs through a ~25 ms clock ramp.  So: wide net,
+    # a pause, then the two inference lines, then the headline's W warmup +
+    # K timed steps, which thereby run at the steady clock of sustained load.
+    S.preload(net)
+    side = {}
+    if world == 1 and not args.no_wide:
+        side["wide"] = wide_training(S)
+        torch.cuda.synchronize()
+        time.sleep(0.5)
+    if world == 1 and not args.no_forward:
+        side["forward_tile_256"] = forward_tile_256(S, net_t)
+        side["forward"] = forward_4k(S, net_t)
     torch.cuda.synchronize()
+    _mark("side legs done")
+
+    for i in range(args.warmup):
+        step()
+        if i == 0:
+            _mark("first warmup step enqueued")
+    torch.cuda.synchronize()
+    _mark("warmup done")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -636,11 +668,7 @@ def main():
         }
         if fwd_sharded is not None:
             out["forward"] = fwd_sharded
-        if world == 1 and not args.no_forward:
-            out["forward"] = forward_4k(S, net_t)
-            out["forward_tile_256"] = forward_tile_256(S, net_t)
-        if world == 1 and not args.no_wide:
-            out["wide"] = wide_training(S)
+        out.update(side)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(net_t, budget_s=args.cpu_budget)
             out["cpu_forward_baseline"] = cpu_forward_baseline(net_t)

@@ -248,6 +248,16 @@ size_t srcnn_net_param_count(const srcnn_net* net) {
   return off[5] + 1;
 }
 
+int srcnn_preload(const srcnn_net* net) {
+  size_t off[6];
+  if (int rc = srcnn_net_offsets(net, off)) return rc;
+  int rc;
+  if ((rc = srcnn::fused::preload(net)) < 0 || (rc = srcnn::fused::preload_forward(net)) < 0 ||
+      (rc = srcnn::wide::preload(net)) < 0)
+    return rc;
+  return srcnn::preload_update();
+}
+
 size_t srcnn_train_workspace_bytes(const srcnn_net* net, uint32_t w, uint32_t h, uint32_t batch) {
   NetDims d;
   if (net_dims(net, w, h, &d) || batch == 0) return 0;

@@ -15,6 +15,17 @@ namespace srcnn {
 int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
 void clear_error();
 
+// hipFuncGetAttributes on each kernel: the runtime's lazy per-device kernel
+// setup happens here instead of at the first launch (srcnn_preload)
+inline int resolve_kernels(const void* const* fns, int n) {
+  for (int i = 0; i < n; i++) {
+    hipFuncAttributes a;
+    hipError_t e = hipFuncGetAttributes(&a, fns[i]);
+    if (e != hipSuccess) return fail(SRCNN_ERR_HIP, "hipFuncGetAttributes: %s", hipGetErrorString(e));
+  }
+  return SRCNN_OK;
+}
+
 inline hipStream_t as_stream(srcnn_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
 
 inline uint32_t grid_for(size_t total, uint32_t block, uint32_t cap = 1u << 20) {

@@ -351,6 +351,20 @@ int forward_clock(double* ghz) {
   return SRCNN_OK;
 }
 
+int preload_forward(const srcnn_net* net) {
+  if (net->f2 != 1) return 0;
+#define SRCNN_FWD_CASE(A, B, C, D)                                                        \
+  if (net->n1 == A && net->n2 == B && net->f1 == C && net->f3 == D) {                    \
+    const void* k[] = {(const void*)fwd_l123_kernel<A, B, C, D>, (const void*)fwd_seam_kernel<D>}; \
+    int rc = resolve_kernels(k, 2);                                                      \
+    return rc ? rc : 1;                                                                  \
+  }
+  SRCNN_FWD_CASE(64, 32, 9, 5)
+  SRCNN_FWD_CASE(32, 16, 9, 5)
+#undef SRCNN_FWD_CASE
+  return 0;
+}
+
 int forward(const srcnn_net* net, const float* X, uint32_t w, uint32_t h, uint32_t batch,
             const float* params, float* out, void* ws, size_t ws_bytes, hipStream_t s,
             bool query_only, size_t* need) {

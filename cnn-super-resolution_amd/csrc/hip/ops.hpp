@@ -64,6 +64,10 @@ struct SlabSeg {
 int reduce_slabs(const SlabSeg* segs, int nseg, hipStream_t s);
 // held-clock probes (common.hpp): slot 0 l12_fwd, 1 l3_delta, 2 d1_grad12
 int train_clock(int slot, double* ghz);
+// srcnn_preload: resolve the family's kernels for this net (1 = this family's
+// net, 0 = not, < 0 error)
+int preload(const srcnn_net* net);
+int preload_forward(const srcnn_net* net);
 int forward_clock(double* ghz);
 }  // namespace fused
 
@@ -76,6 +80,7 @@ int train_fwd_bwd(const srcnn_net* net, const float* X, const float* T, uint32_t
                   uint32_t batch, const float* params, float* grads, float* sq_err, float* A1,
                   float* D1, float* A2, float* D2, float* slab, size_t slab_bytes, hipStream_t s,
                   bool query_only, size_t* need);
+int preload(const srcnn_net* net);
 // op-level launchers of the 5x5 128 <-> 64 middle layer (same contract as
 // the fast::try_* functions: 1 handled, 0 not this shape, < 0 error)
 int op_conv_fwd(const float* in, float* out, const float* W, const float* B, uint32_t in_w,
@@ -104,6 +109,7 @@ int sub_mean(float* d, size_t len, float* mean_out, void* ws, size_t ws_bytes, h
 int fill(float* d, float v, size_t n, hipStream_t s);
 // update_all: the three layers' sgd_update + zero-fill of grads, one launch;
 // off = srcnn_net_offsets(), total = P
+int preload_update();
 int update_all(float* params, float* grads, float* mom, const size_t* off, size_t total,
                const float* lr, float mu, float wd, uint32_t batch, hipStream_t s);
 int extract_luma(const uint8_t* rgba, float* luma, uint32_t w, uint32_t h, int normalize,

@@ -300,6 +300,11 @@ int update_all(float* params, float* grads, float* mom, const size_t* off, size_
   return SRCNN_OK;
 }
 
+int preload_update() {
+  const void* k[] = {(const void*)update_all_kernel};
+  return resolve_kernels(k, 1);
+}
+
 // ---------------------------------------------------------------------------
 // deterministic reductions (sum.cl:35-68, squared_error.cl:36-92):
 // pass 1: fixed grid, per-block tree in LDS -> partial[block]

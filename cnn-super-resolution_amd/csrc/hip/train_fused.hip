@@ -971,6 +971,25 @@ static int dispatch_one(const srcnn_net* net, const float* X, const float* T, ui
                              slab_bytes, s, query_only, need);
 }
 
+template <int N1, int N2, int F1, int F3>
+static int preload_one(const srcnn_net* net) {
+  if (net->n1 != (uint32_t)N1 || net->n2 != (uint32_t)N2 || net->f1 != (uint32_t)F1 ||
+      net->f2 != 1 || net->f3 != (uint32_t)F3)
+    return 0;
+  const void* k[] = {(const void*)l12_fwd_kernel<N1, N2, F1>, (const void*)l3_delta_kernel<N2, F3>,
+                     (const void*)d1_grad12_kernel<N1, N2, F1>, (const void*)slab_reduce_kernel};
+  int rc = resolve_kernels(k, 4);
+  return rc ? rc : 1;
+}
+
+int preload(const srcnn_net* net) {
+  int rc;
+  if ((rc = preload_one<64, 32, 9, 5>(net)) || (rc = preload_one<32, 16, 9, 5>(net)) ||
+      (rc = preload_one<64, 32, 9, 3>(net)) || (rc = preload_one<32, 16, 9, 3>(net)))
+    return rc;
+  return 0;
+}
+
 int train_clock(int slot, double* ghz) {
   unsigned long long a[3][kClockBlocks][2];
   SRCNN_HIP_TRY(hipMemcpyFromSymbol(a, HIP_SYMBOL(g_clk), sizeof(a)));

@@ -1129,6 +1129,18 @@ int op_conv_grad_acc(const float* in, const float* d, float* gW, float* gB, uint
   return 1;
 }
 
+int preload(const srcnn_net* net) {
+  if (!(net->n1 == 128 && net->n2 == 64 && net->f1 == 9 && net->f2 == 5 && net->f3 == 5)) return 0;
+  using NetT = WideNet;
+  const void* k[] = {(const void*)prepack_w2_kernel<128, 64, 5>, (const void*)wl1_fwd_kernel<128, 9>,
+                     (const void*)conv_mfma_kernel<128, 64, 5, NetT::MT2, false, 0>,
+                     (const void*)wl3_kernel<64, 5>,
+                     (const void*)conv_mfma_kernel<64, 128, 5, NetT::MT4, true, 9>,
+                     (const void*)wgrad2_kernel<128, 64, 5>};
+  int rc = resolve_kernels(k, 6);
+  return rc ? rc : 1;
+}
+
 int train_fwd_bwd(const srcnn_net* net, const float* X, const float* T, uint32_t w, uint32_t h,
                   uint32_t batch, const float* params, float* grads, float* sq_err, float* A1,
                   float* D1, float* A2, float* D2, float* slab, size_t slab_bytes, hipStream_t s,

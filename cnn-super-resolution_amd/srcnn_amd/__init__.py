@@ -83,6 +83,7 @@ SIGNATURES = {
     "srcnn_train_workspace_bytes": (_S, [_NP, _U, _U, _U]),
     "srcnn_train_fwd_bwd": (_I, [_NP, _P, _P, _U, _U, _U, _P, _P, _P, _P, _S, _P]),
     "srcnn_update_all": (_I, [_NP, _P, _P, _P, _F, _F, ctypes.POINTER(_F), _U, _P]),
+    "srcnn_preload": (_I, [_NP]),
     "srcnn_forward_workspace_bytes": (_S, [_NP, _U, _U, _U]),
     "srcnn_forward": (_I, [_NP, _P, _U, _U, _U, _P, _P, _P, _S, _P]),
     "srcnn_profile_enable": (_I, [_I]),
@@ -332,6 +333,12 @@ def set_path(p):
 
 def get_path():
     return _lib.srcnn_get_path()
+
+
+def preload(net):
+    """Resolve the net's gfx950 kernels on the current device (srcnn_preload):
+    the runtime's lazy kernel setup happens here, not in the first step."""
+    _call("srcnn_preload", ctypes.byref(net))
 
 
 def last_path():

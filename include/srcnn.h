@@ -166,6 +166,14 @@ typedef struct srcnn_net {
   uint32_t n1, n2, f1, f2, f3; /* Config n1,n2,f1,f2,f3 (src/Config.hpp:27-28) */
 } srcnn_net;
 
+/* Resolve, on the current device, every gfx950 kernel the net-level calls
+ * (srcnn_train_fwd_bwd, srcnn_update_all, srcnn_forward) launch for this net.
+ * No kernel runs.  The HIP runtime otherwise sets a kernel up lazily at its
+ * first launch; resolving them beforehand keeps that out of the first step
+ * (the reference builds its kernels up front too: src/ConfigBasedDataPipeline
+ * .cpp:54-75 create_layer_kernel / create_deltas_kernel at init). */
+SRCNN_API int srcnn_preload(const srcnn_net* net);
+
 /* offsets (in floats) of W1,B1,W2,B2,W3,B3 inside the flat parameter buffer */
 SRCNN_API int srcnn_net_offsets(const srcnn_net* net, size_t offsets[6]);
 SRCNN_API size_t srcnn_net_param_count(const srcnn_net* net);
