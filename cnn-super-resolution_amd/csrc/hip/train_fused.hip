@@ -24,6 +24,7 @@
 // sample -> block -> wave assignment is static and every sum has a fixed
 // order; no float atomics anywhere.
 #include <algorithm>
+#include <type_traits>
 
 #include "common.hpp"
 #include "mfma.hpp"
@@ -784,6 +785,11 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
     }
   }
 }
+#ifndef SRCNN_D1C
+#define SRCNN_D1C 1  // n1 = 64, n2 = 32: kernel 3 in the cooperative-chunk form (d1c.hpp)
+#endif
+#include "d1c.hpp"
+
 // ---------------------------------------------------------------------------
 // deterministic slab reduction: dst[i] += sum_b slab[b][i] in a fixed order
 // ---------------------------------------------------------------------------
@@ -888,7 +894,8 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
       ((ow * oh + 15) / 16 + kL3Threads / 64 - 1) / (kL3Threads / 64) <= L3Lds<N2, F3>::kUnitsPerWave;
   const int g12 = grid_for_batch(batch, SRCNN_L12_GRID);
   const int g3 = grid_for_batch(batch, 256);
-  const int gd = grid_for_batch(batch, 512);
+  const bool kD1c = SRCNN_D1C && N1 == 64 && N2 == 32 && F1 == 9 && d1c_fits(w, h);
+  const int gd = grid_for_batch(batch, kD1c ? kD1cGrid : 512);
   const size_t s12 = (size_t)gd * NetT::P12;
   size_t s3 = (size_t)g3 * NetT::P3, ssq = g3;  // gW3 slabs, squared-error slabs
   if (!l3_fused) {  // the op-level gW3 slabs; the same space serves the squared-error reduction
@@ -943,8 +950,12 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   }
   {
     SRCNN_PROFILE("delta1_grad12_fused", s);
-    hipLaunchKernelGGL((d1_grad12_kernel<N1, N2, F1>), dim3(gd), dim3(256), 0, s, X, A1, D2, W2,
-                       slab12, g);
+    if (kD1c)
+      hipLaunchKernelGGL((d1c_grad12_kernel<(F1 == 9 ? F1 : 9)>), dim3(gd), dim3(256), d1c_lds_bytes(w, h),
+                         s, X, A1, D2, W2, slab12, g, d1c_xs_floats(h));
+    else
+      hipLaunchKernelGGL((d1_grad12_kernel<N1, N2, F1>), dim3(gd), dim3(256), 0, s, X, A1, D2, W2,
+                         slab12, g);
     SRCNN_LAUNCH_TRY();
   }
   {
@@ -977,8 +988,9 @@ static int preload_one(const srcnn_net* net) {
       net->f2 != 1 || net->f3 != (uint32_t)F3)
     return 0;
   const void* k[] = {(const void*)l12_fwd_kernel<N1, N2, F1>, (const void*)l3_delta_kernel<N2, F3>,
-                     (const void*)d1_grad12_kernel<N1, N2, F1>, (const void*)slab_reduce_kernel};
-  int rc = resolve_kernels(k, 4);
+                     (const void*)d1_grad12_kernel<N1, N2, F1>, (const void*)slab_reduce_kernel,
+                     (const void*)d1c_grad12_kernel<9>};
+  int rc = resolve_kernels(k, SRCNN_D1C && N1 == 64 && N2 == 32 && F1 == 9 ? 5 : 4);
   return rc ? rc : 1;
 }
 
