@@ -39,7 +39,11 @@
 // M0 is written by the DMA asm only; the compiler sets it itself around its own uses
 #pragma clang diagnostic ignored "-Winline-asm"
 
-constexpr int kD1cGrid = 1024;  // 256 CUs x 4 resident blocks
+#ifndef SRCNN_D1C_TEAMS
+#define SRCNN_D1C_TEAMS 1  // 4-wave teams per block, on alternate chunks of a sample
+#endif
+constexpr int kD1cTeams = SRCNN_D1C_TEAMS;
+constexpr int kD1cGrid = 1024 / kD1cTeams;  // 256 CUs x 4 waves per SIMD
 constexpr int kD1cS = 40;       // X tile row stride in LDS (8 mod 32)
 constexpr int kD1cMaxPx = 1024; // pixel slots of the X offset table (nch * 32)
 
@@ -70,11 +74,11 @@ __device__ __forceinline__ void d1c_dma4s(const float* base, uint32_t off, float
 inline bool d1c_fits(int w, int h) { return w <= kD1cS && ((w - 8) * (h - 8) + 31) / 32 * 32 <= kD1cMaxPx; }
 inline int d1c_xs_floats(int h) { return (kD1cS * h + 63) / 64 * 64; }
 inline size_t d1c_lds_bytes(int w, int h) {
-  return (size_t)(6144 + 2 * d1c_xs_floats(h) + ((w - 8) * (h - 8) + 31) / 32 * 32) * sizeof(float);
+  return (size_t)(kD1cTeams * 6144 + 2 * d1c_xs_floats(h) + ((w - 8) * (h - 8) + 31) / 32 * 32) * sizeof(float);
 }
 
 template <int F1>
-__global__ __launch_bounds__(256, 4) void d1c_grad12_kernel(const float* __restrict__ X,
+__global__ __launch_bounds__(256 * kD1cTeams, 4) void d1c_grad12_kernel(const float* __restrict__ X,
                                                             const float* __restrict__ A1,
                                                             const float* __restrict__ D2,
                                                             const float* __restrict__ W2,
@@ -83,13 +87,15 @@ __global__ __launch_bounds__(256, 4) void d1c_grad12_kernel(const float* __restr
   static_assert(F1 == 9, "d1c: the tap tiling is for 9x9 layer-1 filters");
   constexpr int K1 = F1 * F1, NW1 = K1 * N1, NW2 = N1 * N2, P12 = NW1 + N1 + NW2 + N2;
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* const a1i = smem;         // [2 buffers][4 waves][512]
-  float* const d2i = smem + 4096;  // [2 buffers][1024]
-  float* const xsi = smem + 6144;  // [2 samples][xsf]
-  int* const xo = reinterpret_cast<int*>(smem + 6144 + 2 * xsf);  // [nch * 32] pixel -> X offset
+  constexpr int NT = kD1cTeams;
+  const int lane = mfma::lane_id(), wv = mfma::wave_id();
+  const int team = wv >> 2, wave = wv & 3;  // team t takes chunks t, t + NT, ...
+  float* const a1i = smem + team * 6144;         // per team: [2 buffers][4 waves][512]
+  float* const d2i = smem + team * 6144 + 4096;  // per team: [2 buffers][1024]
+  float* const xsi = smem + NT * 6144;           // [2 samples][xsf]
+  int* const xo = reinterpret_cast<int*>(xsi + 2 * xsf);  // [nch * 32] pixel -> X offset
 
   SRCNN_CLOCK_BEGIN();
-  const int lane = mfma::lane_id(), wave = mfma::wave_id();
   const int lq = lane & 15, lg = lane >> 4;
   const int c0 = 16 * wave;
   const int npx = g.ow * g.oh, nch = (npx + 31) / 32;
@@ -165,7 +171,7 @@ __global__ __launch_bounds__(256, 4) void d1c_grad12_kernel(const float* __restr
   // X tile of sample smp -> dst at row stride S (pad slots read a clamped pixel)
   auto dma_x = [&](int smp, float* dst) {
     const float* xsrc = X + (size_t)smp * g.W * g.H;
-    for (int k = wave; 64 * k < S * g.H; k += 4) {
+    for (int k = wv; 64 * k < S * g.H; k += 4 * NT) {
       int l_ = lane;
       asm volatile("" : "+v"(l_));
       const int f = 64 * k + l_, r = f / S;
@@ -176,21 +182,23 @@ __global__ __launch_bounds__(256, 4) void d1c_grad12_kernel(const float* __restr
   int buf = 0, xbuf = 0;
   if ((int)blockIdx.x < g.batch) {
     dma_x(blockIdx.x, xsi);
-    dma_chunk(blockIdx.x, 0, 0);
+    if (team < nch) dma_chunk(blockIdx.x, team, 0);
   }
   for (int smp = blockIdx.x; smp < g.batch; smp += gridDim.x, xbuf ^= 1) {
     const int next = smp + (int)gridDim.x;
     const float* xs = xsi + xbuf * xsf;
-    for (int c = 0; c < nch; c++, buf ^= 1) {
-      // this chunk's operands (and at c == 0 this sample's X tile) have
+    for (int cc = 0; cc < nch; cc += NT, buf ^= 1) {
+      // this chunk's operands (and at cc == 0 this sample's X tile) have
       // landed for every wave; every wave is done with the other buffer
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      if (c + 1 < nch)
-        dma_chunk(smp, c + 1, buf ^ 1);
-      else if (next < g.batch)
-        dma_chunk(next, 0, buf ^ 1);
-      if (c == 0 && next < g.batch) dma_x(next, xsi + (xbuf ^ 1) * xsf);
+      const int c = cc + team;
+      if (c + NT < nch)
+        dma_chunk(smp, c + NT, buf ^ 1);
+      else if (next < g.batch && team < nch)
+        dma_chunk(next, team, buf ^ 1);
+      if (cc == 0 && next < g.batch) dma_x(next, xsi + (xbuf ^ 1) * xsf);
+      if (c >= nch) continue;  // odd chunk count: this team idles on the last step
       const float* d2b = d2i + buf * 1024;
       const float* a1b = a1i + (buf * 4 + wave) * 512;
 
@@ -254,6 +262,39 @@ __global__ __launch_bounds__(256, 4) void d1c_grad12_kernel(const float* __restr
     }
   }
   SRCNN_CLOCK_END(g_clk, 2);
+  if constexpr (NT == 2) {
+    // team 1 parks its partial gradients in LDS, team 0 adds them (fixed order)
+    __syncthreads();
+    float* red = smem + wave * 32 * 64 + lane;
+    if (team == 1) {
+#pragma unroll
+      for (int m = 0; m < 5; m++)
+#pragma unroll
+        for (int i = 0; i < 4; i++) red[(4 * m + i) * 64] = g1[m][i];
+#pragma unroll
+      for (int u = 0; u < 2; u++)
+#pragma unroll
+        for (int i = 0; i < 4; i++) red[(20 + 4 * u + i) * 64] = g2[u][i];
+      red[28 * 64] = gv;
+      red[29 * 64] = gvb;
+      red[30 * 64] = gb2[0];
+      red[31 * 64] = gb2[1];
+    }
+    __syncthreads();
+    if (team == 1) return;
+#pragma unroll
+    for (int m = 0; m < 5; m++)
+#pragma unroll
+      for (int i = 0; i < 4; i++) g1[m][i] += red[(4 * m + i) * 64];
+#pragma unroll
+    for (int u = 0; u < 2; u++)
+#pragma unroll
+      for (int i = 0; i < 4; i++) g2[u][i] += red[(20 + 4 * u + i) * 64];
+    gv += red[28 * 64];
+    gvb += red[29 * 64];
+    gb2[0] += red[30 * 64];
+    gb2[1] += red[31 * 64];
+  }
 
   // slab of this block: [gW1 | gB1 | gW2 | gB2]; every wave writes its channels.
   // Row 4 lg + i of tile m is the A-operand lane lq' = 4 lg + i, i.e. tap

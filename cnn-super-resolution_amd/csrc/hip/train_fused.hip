@@ -816,8 +816,18 @@ __global__ __launch_bounds__(1024) void slab_reduce_kernel(SlabSegs ss) {
   const int col = ((int)blockIdx.x - ss.first[k]) * kSlabCols + cl;
   const size_t stride = sg.stride ? sg.stride : sg.P;
   float acc = 0.0f;
-  if (col < sg.P)
-    for (int b = row; b < sg.nslab; b += kSlabRows) acc += sg.slab[(size_t)b * stride + col];
+  if (col < sg.P) {
+    // 8 loads in flight per thread, summed in slab order
+    int b = row;
+    for (; b + 7 * kSlabRows < sg.nslab; b += 8 * kSlabRows) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; j++) v[j] = sg.slab[(size_t)(b + j * kSlabRows) * stride + col];
+#pragma unroll
+      for (int j = 0; j < 8; j++) acc += v[j];
+    }
+    for (; b < sg.nslab; b += kSlabRows) acc += sg.slab[(size_t)b * stride + col];
+  }
   part[row][cl] = acc;
   __syncthreads();
   if (row == 0 && col < sg.P) {
@@ -951,7 +961,7 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   {
     SRCNN_PROFILE("delta1_grad12_fused", s);
     if (kD1c)
-      hipLaunchKernelGGL((d1c_grad12_kernel<(F1 == 9 ? F1 : 9)>), dim3(gd), dim3(256), d1c_lds_bytes(w, h),
+      hipLaunchKernelGGL((d1c_grad12_kernel<(F1 == 9 ? F1 : 9)>), dim3(gd), dim3(256 * kD1cTeams), d1c_lds_bytes(w, h),
                          s, X, A1, D2, W2, slab12, g, d1c_xs_floats(h));
     else
       hipLaunchKernelGGL((d1_grad12_kernel<N1, N2, F1>), dim3(gd), dim3(256), 0, s, X, A1, D2, W2,
