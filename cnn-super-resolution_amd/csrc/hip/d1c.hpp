@@ -43,6 +43,13 @@
 #define SRCNN_D1C_TEAMS 1  // 4-wave teams per block, on alternate chunks of a sample
 #endif
 constexpr int kD1cTeams = SRCNN_D1C_TEAMS;
+// diagnostics builds only (results invalid): 1 no chunk barrier, 2 no chunk
+// operand DMA, 4 gW1 A operands from a register (no X gathers), 8 no relu' reads
+#ifdef SRCNN_D1C_DIAG
+constexpr int kD1cDiag = SRCNN_D1C_DIAG;
+#else
+constexpr int kD1cDiag = 0;
+#endif
 constexpr int kD1cGrid = 1024 / kD1cTeams;  // 256 CUs x 4 waves per SIMD
 constexpr int kD1cS = 40;       // X tile row stride in LDS (8 mod 32)
 constexpr int kD1cMaxPx = 1024; // pixel slots of the X offset table (nch * 32)
@@ -191,9 +198,10 @@ __global__ __launch_bounds__(256 * kD1cTeams, 4) void d1c_grad12_kernel(const fl
       // this chunk's operands (and at cc == 0 this sample's X tile) have
       // landed for every wave; every wave is done with the other buffer
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
+      if (!(kD1cDiag & 1) || cc == 0) __syncthreads();
       const int c = cc + team;
-      if (c + NT < nch)
+      if (kD1cDiag & 2) {
+      } else if (c + NT < nch)
         dma_chunk(smp, c + NT, buf ^ 1);
       else if (next < g.batch && team < nch)
         dma_chunk(next, team, buf ^ 1);
@@ -202,6 +210,15 @@ __global__ __launch_bounds__(256 * kD1cTeams, 4) void d1c_grad12_kernel(const fl
       const float* d2b = d2i + buf * 1024;
       const float* a1b = a1i + (buf * 4 + wave) * 512;
 
+      // relu' operands of layer 1 first (A1 > 0; register i of d1[pm] below is
+      // pixel 16 pm + 4 lg + i), so their LDS latency hides under delta1 and
+      // gW2 (read just before the mask, they cost 3% of the kernel)
+      float mk[2][4];
+#pragma unroll
+      for (int pm = 0; pm < 2; pm++)
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+          mk[pm][i] = (kD1cDiag & 8) ? 1.0f : a1b[256 * pm + 16 * i + ((i & 1) ? r4o : r4e)];
       // delta1 (its operands: two 16-B reads per pixel tile)
       f32x4 av[2][2], d1[2];
 #pragma unroll
@@ -210,37 +227,30 @@ __global__ __launch_bounds__(256 * kD1cTeams, 4) void d1c_grad12_kernel(const fl
         av[pm][1] = *reinterpret_cast<const f32x4*>(d2b + 512 * pm + r1b1);
         d1[pm] = mfma::zero4();
       }
+      __builtin_amdgcn_sched_barrier(0);  // keep the reads above issued first
 #pragma unroll
       for (int s = 0; s < 8; s++)
 #pragma unroll
         for (int pm = 0; pm < 2; pm++) d1[pm] = mfma::mma16(av[pm][s >> 2][s & 3], w2r[s], d1[pm]);
 
-      // gW2 += A1^T delta2 (k-step s: pixel 4 s + pl); gB2 in wave 0 only
-      auto gw2 = [&](auto with_gb2) {
+      // gW2 += A1^T delta2 (k-step s: pixel 4 s + pl)
 #pragma unroll
-        for (int s = 0; s < 8; s++) {
-          const float a = a1b[64 * s + r3b[s & 1]];
+      for (int s = 0; s < 8; s++) {
+        const float a = a1b[64 * s + r3b[s & 1]];
 #pragma unroll
-          for (int u = 0; u < 2; u++) {
-            const float b = d2b[128 * s + r2b[u][s & 1]];
-            g2[u] = mfma::mma16(a, b, g2[u]);
-            if constexpr (decltype(with_gb2)::value) gb2[u] += b;
-          }
-        }
-      };
-      if (wave == 0)
-        gw2(std::true_type{});
-      else
-        gw2(std::false_type{});
+        for (int u = 0; u < 2; u++) g2[u] = mfma::mma16(a, d2b[128 * s + r2b[u][s & 1]], g2[u]);
+      }
+      // gB2 += delta2: wave w sums k-steps 2w, 2w + 1 (balanced; the waves
+      // meet at every chunk barrier), the waves' partials are added at the end
+#pragma unroll
+      for (int u = 0; u < 2; u++)
+        gb2[u] += d2b[256 * wave + r2b[u][0]] + d2b[256 * wave + 128 + r2b[u][1]];
 
-      // relu' of layer 1: register i of d1[pm] is pixel 16 pm + 4 lg + i
+      // relu' of layer 1
 #pragma unroll
       for (int pm = 0; pm < 2; pm++)
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
-          const float m = a1b[256 * pm + 16 * i + ((i & 1) ? r4o : r4e)];
-          d1[pm][i] = m > 0.0f ? d1[pm][i] : 0.0f;
-        }
+        for (int i = 0; i < 4; i++) d1[pm][i] = mk[pm][i] > 0.0f ? d1[pm][i] : 0.0f;
 
       // gW1 += Xwin^T delta1: k-step (pm, i), lane group lg <-> pixel 16 pm + 4 lg + i
       // (pixels past the sample map onto its last one: their delta1 is 0)
@@ -252,9 +262,14 @@ __global__ __launch_bounds__(256 * kD1cTeams, 4) void d1c_grad12_kernel(const fl
           const int xb = i == 0 ? xb4.x : i == 1 ? xb4.y : i == 2 ? xb4.z : xb4.w;
           const float bv = d1[pm][i];
           const float* xl = xs + xb;
+          if (kD1cDiag & 4) {
 #pragma unroll
-          for (int m = 0; m < 4; m++) g1[m] = mfma::mma16(xl[tb + kTileOff[m]], bv, g1[m]);
-          g1[4] = mfma::mma16(xl[t4], bv, g1[4]);
+            for (int m = 0; m < 5; m++) g1[m] = mfma::mma16(bv + m, bv, g1[m]);
+          } else {
+#pragma unroll
+            for (int m = 0; m < 4; m++) g1[m] = mfma::mma16(xl[tb + kTileOff[m]], bv, g1[m]);
+            g1[4] = mfma::mma16(xl[t4], bv, g1[4]);
+          }
           gv = fmaf(xl[7 * S + 8], bv, gv);
           gvb += bv;
         }
@@ -281,7 +296,6 @@ __global__ __launch_bounds__(256 * kD1cTeams, 4) void d1c_grad12_kernel(const fl
       red[31 * 64] = gb2[1];
     }
     __syncthreads();
-    if (team == 1) return;
 #pragma unroll
     for (int m = 0; m < 5; m++)
 #pragma unroll
@@ -300,6 +314,8 @@ __global__ __launch_bounds__(256 * kD1cTeams, 4) void d1c_grad12_kernel(const fl
   // Row 4 lg + i of tile m is the A-operand lane lq' = 4 lg + i, i.e. tap
   // (dy0 + lg, dx0 + i) for tiles 0-3.
   float* out = slab + (size_t)blockIdx.x * P12;
+  const bool writer = team == 0;  // (two teams: team 0 holds the sums)
+  if (writer)
 #pragma unroll
   for (int m = 0; m < 4; m++)
 #pragma unroll
@@ -307,6 +323,7 @@ __global__ __launch_bounds__(256 * kD1cTeams, 4) void d1c_grad12_kernel(const fl
       const int tap = (4 * (m >> 1) + lg) * F1 + 4 * (m & 1) + i;
       out[tap * N1 + c0 + lq] = g1[m][i];
     }
+  if (writer)
 #pragma unroll
   for (int i = 0; i < 4; i++) {
     const int l4 = 4 * lg + i;
@@ -319,16 +336,31 @@ __global__ __launch_bounds__(256 * kD1cTeams, 4) void d1c_grad12_kernel(const fl
   };
   {
     const float v = lg_sum(gv), vb = lg_sum(gvb);
-    if (lg == 0) {
+    if (writer && lg == 0) {
       out[(7 * F1 + 8) * N1 + c0 + lq] = v;
       out[NW1 + c0 + lq] = vb;
     }
   }
+  if (writer)
 #pragma unroll
-  for (int u = 0; u < 2; u++) {
+  for (int u = 0; u < 2; u++)
 #pragma unroll
     for (int i = 0; i < 4; i++) out[NW1 + N1 + (c0 + 4 * lg + i) * N2 + 16 * u + lq] = g2[u][i];
+  // gB2: the waves' partials in wave order (LDS past the two-team exchange area)
+  float* const red2 = smem + (NT == 2 ? 8192 : 0);
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < 2; u++) {
     const float v = lg_sum(gb2[u]);
-    if (wave == 0 && lg == 0) out[NW1 + N1 + NW2 + 16 * u + lq] = v;
+    if (writer && lg == 0) red2[(wave * 2 + u) * 16 + lq] = v;
   }
+  __syncthreads();
+  if (writer && wave == 0 && lg == 0)
+#pragma unroll
+    for (int u = 0; u < 2; u++) {
+      float v = 0.0f;
+#pragma unroll
+      for (int w = 0; w < 4; w++) v += red2[(w * 2 + u) * 16 + lq];
+      out[NW1 + N1 + NW2 + 16 * u + lq] = v;
+    }
 }
