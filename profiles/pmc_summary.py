@@ -21,6 +21,7 @@ SHORT = [
     (r"l12_fwd_kernel", "l12_fwd_mfma"),
     (r"l3_delta_kernel", "l3_delta_fused"),
     (r"d1_grad12_kernel", "delta1_grad12_fused"),
+    (r"d1c_grad12_kernel", "delta1_grad12_fused"),
     (r"slab_reduce_kernel", "slab_reduce"),
     (r"fwd_l123_kernel", "fwd_l123_mfma"),
     (r"fwd_seam_kernel", "fwd_l3_seam"),
