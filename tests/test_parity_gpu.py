@@ -377,12 +377,22 @@ def expected_train_path(name, size, path):
     return {"generic", "fast"}
 
 
+def test_preload_every_net(S):
+    """srcnn_preload resolves the net-level kernels of every net family (and
+    is a no-op for nets without specialised kernels); a step afterwards runs."""
+    for cfg in NETS.values():
+        S.preload(S.Net(*cfg))
+    assert S.lib().srcnn_preload(None) != 0  # null net: SRCNN_ERR_INVALID, no crash
+
+
 @pytest.mark.parametrize("name,batch,size", [("default", 16, 33), ("wide", 3, 33), ("tiny", 5, 15),
                                              ("default", 2, 48), ("example", 7, 33),
                                              ("default", 3, 21), ("default", 600, 33),
                                              # ragged against the grids: l3 (256 blocks, walks the
                                              # batch from its end), l12 / d1 (512 blocks)
                                              ("default", 257, 33), ("default", 513, 33),
+                                             # d1c (1024 blocks, 4 samples each at batch 4096)
+                                             ("default", 1025, 33), ("default", 5, 39),
                                              # tiles past l3_delta's LDS image (33x33): l12 +
                                              # op-level layer 3 + d1; 36x36 as the reference's
                                              # train_samples36 (profile.py:7)
