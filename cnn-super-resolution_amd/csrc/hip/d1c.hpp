@@ -50,7 +50,13 @@ constexpr int kD1cDiag = SRCNN_D1C_DIAG;
 #else
 constexpr int kD1cDiag = 0;
 #endif
-constexpr int kD1cGrid = 1024 / kD1cTeams;  // 256 CUs x 4 waves per SIMD
+#ifndef SRCNN_D1C_OCC
+#define SRCNN_D1C_OCC 4  // waves per SIMD (launch bound; register budget 512 / this)
+#endif
+#ifndef SRCNN_D1C_GRID
+#define SRCNN_D1C_GRID (256 * SRCNN_D1C_OCC / SRCNN_D1C_TEAMS)  // all blocks resident
+#endif
+constexpr int kD1cGrid = SRCNN_D1C_GRID;
 constexpr int kD1cS = 40;       // X tile row stride in LDS (8 mod 32)
 constexpr int kD1cMaxPx = 1024; // pixel slots of the X offset table (nch * 32)
 
@@ -85,7 +91,7 @@ inline size_t d1c_lds_bytes(int w, int h) {
 }
 
 template <int F1>
-__global__ __launch_bounds__(256 * kD1cTeams, 4) void d1c_grad12_kernel(const float* __restrict__ X,
+__global__ __launch_bounds__(256 * kD1cTeams, SRCNN_D1C_OCC) void d1c_grad12_kernel(const float* __restrict__ X,
                                                             const float* __restrict__ A1,
                                                             const float* __restrict__ D2,
                                                             const float* __restrict__ W2,
