@@ -442,6 +442,31 @@ def test_train_step_vs_oracle(S, path, name, batch, size):
     assert not H(g_ref_dev).any()
 
 
+@pytest.mark.parametrize("w,h,batch", [(35, 31, 7), (29, 38, 5), (33, 17, 9)])
+def test_train_step_nonsquare_tiles(S, w, h, batch):
+    """Non-square training tiles through the fused kernels (l12, l3 / op-level
+    layer 3, d1c: pixel -> X offsets and row clamps use ow != oh)."""
+    cfg = NETS["default"]
+    net = S.Net(*cfg)
+    rng = np.random.default_rng(7)
+    X, T = make_batch(rng, batch, w, h)
+    params = make_params(rng, cfg, sd=0.05)
+    P = params.size
+    g0 = np.zeros(P, np.float32)
+    rg, _ = orc.train_fwd_bwd(cfg, X, T, w, h, batch, params, g0)
+    xg, _ = orc.f64.train_fwd_bwd(cfg, X, T, w, h, batch, params, g0)
+    nbytes = S.train_workspace_bytes(net, w, h, batch)
+    ws = torch.empty(nbytes // 4 + 64, dtype=torch.float32, device="cuda")
+    g = D(g0)
+    S.train_fwd_bwd(net, D(X), D(T), w, h, batch, D(params), g, None, ws, nbytes)
+    assert S.last_path() == "fused", S.last_path()
+    got = H(g)
+    off = S.net_offsets(net) + [P]
+    for i, nm in enumerate(["W1", "B1", "W2", "B2", "W3", "B3"]):
+        sl = slice(off[i], off[i + 1])
+        assert_close(got[sl], rg[sl], RTOL, "grad " + nm, xg[sl], FLIP_FLOOR)
+
+
 def test_forward_vs_oracle(S, path):
     cfg = NETS["default"]
     net = S.Net(*cfg)
