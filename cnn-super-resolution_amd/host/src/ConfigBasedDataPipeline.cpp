@@ -76,6 +76,12 @@ void ConfigBasedDataPipeline::load_kernels(int load_flags) {
     _allreduce_kernel = _context->create_kernel(KernelKind::AllReduce, "srcnn_allreduce_grads", 0, 0, 0,
                                                 false, net_args);
   }
+  // the net-level gfx950 kernels are set up here, as the reference builds its
+  // kernels at init (src/ConfigBasedDataPipeline.cpp:54-75), not in the first batch
+  if (load_flags & (LOAD_KERNEL_LAYERS | LOAD_KERNEL_BACKPROPAGATE)) {
+    srcnn_net nt = net();
+    check(srcnn_preload(&nt), "srcnn_preload");
+  }
 }
 
 void ConfigBasedDataPipeline::set_mini_batch_size(size_t n) {
