@@ -86,6 +86,11 @@ constexpr bool kL3DirectD2 = true;
 constexpr bool kL3DirectD2 = false;
 #endif
 constexpr int kL3MaxOut = kL3TPF * kL3Threads;
+// units per wave whose masked delta2 is held for the next sample's Q phase
+// (the others are stored straight from the delta2 phase); default: all
+#ifndef SRCNN_L3_DEFER
+#define SRCNN_L3_DEFER 99
+#endif
 
 // float index of A2[p][n] in the swizzled LDS image
 template <int N2>
@@ -308,7 +313,7 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
         for (int s = 0; s < KQ; s++)
 #pragma unroll
           for (int t = 0; t < TT; t++) acc[t] = mfma::mma16(av[s], wq[s][t], acc[t]);
-        if (!kL3DirectD2) SRCNN_L3_D2_STORE(j);
+        if (!kL3DirectD2 && j < SRCNN_L3_DEFER) SRCNN_L3_D2_STORE(j);
         // Q[u0 + 4lg + i][tap = 16t + lq] (the region holds whole units: rows
         // past the sample are written too, never read)
 #pragma unroll
@@ -405,7 +410,7 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
 #pragma unroll
             for (int t = 0; t < NT; t++)
               gacc[t3][t] = mfma::mma16(ag[s][t3], bg[s][t], gacc[t3][t]);
-        if constexpr (kL3DirectD2) {
+        if (kL3DirectD2 || j >= SRCNN_L3_DEFER) {
           const int q_ = u0 + lq;
           if (q_ < npx2 && !kL3DiagNoStore) {
             float* dst_ = D2 + ((size_t)l3_order(sample, g.batch) * npx2 + q_) * N2 + 4 * lg;
@@ -432,7 +437,8 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
   }
   if (!kL3DirectD2)
 #pragma unroll
-    for (int j = 0; j < kUMax; j++) SRCNN_L3_D2_STORE(j);
+    for (int j = 0; j < kUMax; j++)
+      if (j < SRCNN_L3_DEFER) SRCNN_L3_D2_STORE(j);
 #undef SRCNN_L3_D2_STORE
 #undef SRCNN_L3_A2_DMA
   SRCNN_CLOCK_END(g_clk, 1);
