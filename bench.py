@@ -554,15 +554,21 @@ def main():
     # launched on an idle GPU runs through a ~25 ms clock ramp.  So: wide net,
     # a pause, then the two inference lines, then the headline's W warmup +
     # K timed steps, which thereby run at the steady clock of sustained load.
+    # With N > 1 every rank runs the same sequence on its own GPU, so that each
+    # N's headline starts from the same power state (a rank that skipped it
+    # would time its warmup through the idle clock ramp and the scaling curve
+    # would charge that to N); only N = 1 reports these lines.
     S.preload(net)
     side = {}
-    if world == 1 and not args.no_wide:
+    if not args.no_wide:
         side["wide"] = wide_training(S)
         torch.cuda.synchronize()
         time.sleep(0.5)
-    if world == 1 and not args.no_forward:
+    if not args.no_forward:
         side["forward_tile_256"] = forward_tile_256(S, net_t)
         side["forward"] = forward_4k(S, net_t)
+    if world > 1:
+        side = {}
     torch.cuda.synchronize()
     _mark("side legs done")
 
