@@ -447,7 +447,7 @@ def wide_training(S, steps=5, warmup=2, batch=4096):
                for k, (c, t) in stats.items()}
     rooflines = {}
     for k, (c, t) in stats.items():
-        r = roofline_of(k, c / steps, t / steps, work, batch, None, net_t, w, h)
+        r = roofline_of(k, c / steps, t / steps, work, batch, load_pmc(), net_t, w, h)
         if r:
             rooflines[k] = r
     return {"workload": "SRCNN wide n1=128 n2=64 f1=9 f2=5 f3=5, fp32 training, 33x33 tiles, "
