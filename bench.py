@@ -545,6 +545,13 @@ def main():
         lambda g: S.train_fwd_bwd(net, Xd, Td, w, h, B, params, g, None, ws, ws_bytes, stream),
         lambda nb: S.update_all(net, params, grads, mom, 0.9, 1e-3, lr, nb, stream),
         global_tiles, allreduce=comm)
+    if world == 1 and not os.environ.get("SRCNN_BENCH_SEPARATE_UPDATE"):
+        # one device, no exchange: srcnn_train_step (the same step; on the
+        # fused path the update runs inside the gradient reduction).
+        # SRCNN_BENCH_SEPARATE_UPDATE=1: fwd_bwd + update_all (A/B)
+        def step():
+            S.train_step(net, Xd, Td, w, h, B, params, grads, mom, 0.9, 1e-3, lr, global_tiles,
+                         None, ws, ws_bytes, stream)
 
     # The single-GPU side lines (the wide net, one 256x256 tile, 4K inference)
     # are measured before the headline.  Order and pause matter on this part

@@ -285,9 +285,12 @@ size_t srcnn_train_workspace_bytes(const srcnn_net* net, uint32_t w, uint32_t h,
   return b + align_up(g);
 }
 
-int srcnn_train_fwd_bwd(const srcnn_net* net, const float* X, const float* T, uint32_t w,
-                        uint32_t h, uint32_t batch, const float* params, float* grads,
-                        float* sq_err, void* ws, size_t ws_bytes, srcnn_stream_t stream) {
+// srcnn_train_fwd_bwd, and with `up` srcnn_train_step's fused variant:
+// *updated = true when the fused slab reduction also applied the update
+static int train_impl(const srcnn_net* net, const float* X, const float* T, uint32_t w,
+                      uint32_t h, uint32_t batch, const float* params, float* grads,
+                      float* sq_err, void* ws, size_t ws_bytes, srcnn_stream_t stream,
+                      const srcnn::fused::SlabUpdate* up, bool* updated) {
   NetDims d;
   if (int rc = net_dims(net, w, h, &d)) return rc;
   if (batch == 0) return SRCNN_OK;
@@ -320,7 +323,8 @@ int srcnn_train_fwd_bwd(const srcnn_net* net, const float* X, const float* T, ui
   if (fast_enabled()) {
     rc = srcnn::fused::train_fwd_bwd(net, X, T, w, h, batch, params, grads, sq_err, A1, A2, D2, A3,
                                      D3, static_cast<float*>(gws), gws_bytes,
-                                     srcnn::as_stream(stream), false, nullptr);
+                                     srcnn::as_stream(stream), false, nullptr, up);
+    if (rc == 2 && updated) *updated = true;
     if (rc != 0) return rc < 0 ? rc : tag("fused", SRCNN_OK);
     rc = srcnn::wide::train_fwd_bwd(net, X, T, w, h, batch, params, grads, sq_err, A1, D1, A2, D2,
                                     static_cast<float*>(gws), gws_bytes, srcnn::as_stream(stream),
@@ -352,6 +356,40 @@ int srcnn_train_fwd_bwd(const srcnn_net* net, const float* X, const float* T, ui
     return rc;
   return seq.done(srcnn_conv_grad_acc(X, D1, gW1, gB1, 1, net->n1, net->f1, d.w1, d.h1, batch, gws,
                                       gws_bytes, stream));
+}
+
+int srcnn_train_fwd_bwd(const srcnn_net* net, const float* X, const float* T, uint32_t w,
+                        uint32_t h, uint32_t batch, const float* params, float* grads,
+                        float* sq_err, void* ws, size_t ws_bytes, srcnn_stream_t stream) {
+  return train_impl(net, X, T, w, h, batch, params, grads, sq_err, ws, ws_bytes, stream, nullptr,
+                    nullptr);
+}
+
+int srcnn_train_step(const srcnn_net* net, const float* X, const float* T, uint32_t w, uint32_t h,
+                     uint32_t batch, float* params, float* grads, float* momentum_bufs,
+                     float momentum, float wd, const float* lr, uint32_t update_batch,
+                     float* sq_err, void* ws, size_t ws_bytes, srcnn_stream_t stream) {
+  SRCNN_REQUIRE(net && params && grads && momentum_bufs && lr, "train_step: null argument");
+  size_t off[6];
+  if (int rc = srcnn_net_offsets(net, off)) return rc;
+  const size_t total = off[5] + 1;
+  SRCNN_REQUIRE(total < (1ull << 32), "train_step: parameter count %zu too large", total);
+  srcnn::fused::SlabUpdate u{};
+  u.P = params;
+  u.G = grads;
+  u.M = momentum_bufs;
+  for (int k = 0; k < 6; k++) u.off[k] = (uint32_t)off[k];
+  u.off[6] = (uint32_t)total;
+  for (int k = 0; k < 3; k++) u.lr[k] = lr[k];
+  u.mu = momentum;
+  u.wd = wd;
+  u.batch = (float)update_batch;
+  bool updated = false;
+  if (int rc = train_impl(net, X, T, w, h, batch, params, grads, sq_err, ws, ws_bytes, stream, &u,
+                          &updated))
+    return rc;
+  if (updated) return SRCNN_OK;
+  return srcnn_update_all(net, params, grads, momentum_bufs, momentum, wd, lr, update_batch, stream);
 }
 
 int srcnn_update_all(const srcnn_net* net, float* params, float* grads, float* momentum_bufs,

@@ -42,10 +42,14 @@ int try_conv_grad_acc(const float* in, const float* d, float* gW, float* gB, uin
 // Returns 1 when the net/shape is specialised (step enqueued, or with
 // query_only the slab workspace size written to *need), 0 when not.
 namespace fused {
+struct SlabUpdate;
+// With `up` (srcnn_train_step) the slab reduction also applies the SGD
+// update to every parameter it completes and returns 2 instead of 1 when it
+// did (layer 3 on l3_delta, so the slabs cover all parameters).
 int train_fwd_bwd(const srcnn_net* net, const float* X, const float* T, uint32_t w, uint32_t h,
                   uint32_t batch, const float* params, float* grads, float* sq_err, float* A1,
                   float* A2, float* D2, float* A3, float* D3, float* slab, size_t slab_bytes,
-                  hipStream_t s, bool query_only, size_t* need);
+                  hipStream_t s, bool query_only, size_t* need, const SlabUpdate* up = nullptr);
 // Fused inference (forward_fused.hip): 1 when specialised (with query_only:
 // workspace bytes in *need), 0 when not.
 int forward(const srcnn_net* net, const float* X, uint32_t w, uint32_t h, uint32_t batch,
@@ -61,7 +65,36 @@ struct SlabSeg {
   int nslab, P;
   int stride;  // floats between consecutive slabs (0 = P)
 };
-int reduce_slabs(const SlabSeg* segs, int nseg, hipStream_t s);
+// Optional SGD update fused into the reduction (srcnn_train_step): segments
+// k < nseg of `up` are parameter gradients inside the flat buffer G; element
+// i = dst - G + col gets g = G[i] + sum, then sgd_step (same arithmetic as
+// update_all) on P[i] / M[i], and G[i] = 0.
+struct SlabUpdate {
+  float *P, *G, *M;
+  uint32_t off[7];  // [W1|B1|W2|B2|W3|B3] offsets, off[6] = total
+  float lr[3];
+  float mu, wd, batch;
+  int nseg;
+};
+int reduce_slabs(const SlabSeg* segs, int nseg, hipStream_t s, const SlabUpdate* up = nullptr);
+// SGD-momentum step of one parameter (update_parameters.cl:14-32): segment
+// seg of [W1|B1|W2|B2|W3|B3], weights with weight decay, biases without;
+// w, m = parameter and momentum in, out.  Shared by update_all_kernel and the
+// fused reduction so both round alike.
+__device__ __forceinline__ void sgd_step(float& w, float& m, int seg, float g, float lr, float mu,
+                                         float wd, float batch) {
+  // no FMA contraction: both call sites must round identically
+#pragma clang fp contract(off)
+  if ((seg & 1) == 0) {
+    const float dw = mu * m + lr * g + wd * w;
+    w = w - dw / batch;
+    m = dw;
+  } else {
+    const float db = mu * m + lr * g;
+    w -= db / batch;
+    m = db;
+  }
+}
 // held-clock probes (common.hpp): slot 0 l12_fwd, 1 l3_delta, 2 d1_grad12
 int train_clock(int slot, double* ghz);
 // srcnn_preload: resolve the family's kernels for this net (1 = this family's

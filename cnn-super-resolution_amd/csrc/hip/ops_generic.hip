@@ -271,18 +271,11 @@ __global__ void update_all_kernel(float* __restrict__ P, float* __restrict__ G,
     int seg = 0;
 #pragma unroll
     for (int k = 1; k < 6; k++) seg += i >= sg.off[k];
-    const float lr = sg.lr[seg >> 1];
-    const float g = G[i];
-    if ((seg & 1) == 0) {  // weights: update_parameters.cl:14-24
-      const float w = P[i];
-      const float dw = mu * M[i] + lr * g + wd * w;
-      P[i] = w - dw / batch;
-      M[i] = dw;
-    } else {  // biases, no weight decay: update_parameters.cl:26-32
-      const float db = mu * M[i] + lr * g;
-      P[i] -= db / batch;
-      M[i] = db;
-    }
+    // weights: update_parameters.cl:14-24; biases, no weight decay: :26-32
+    float w = P[i], m = M[i];
+    fused::sgd_step(w, m, seg, G[i], sg.lr[seg >> 1], mu, wd, batch);
+    P[i] = w;
+    M[i] = m;
     G[i] = 0.0f;
   }
 }

@@ -805,6 +805,7 @@ constexpr int kSlabRows = 1024 / kSlabCols;
 struct SlabSegs {
   SlabSeg seg[kMaxSlabSegs];
   int first[kMaxSlabSegs + 1];
+  SlabUpdate up;  // up.nseg = 0: plain reduction
 };
 
 __global__ __launch_bounds__(1024) void slab_reduce_kernel(SlabSegs ss) {
@@ -815,6 +816,16 @@ __global__ __launch_bounds__(1024) void slab_reduce_kernel(SlabSegs ss) {
   const int cl = threadIdx.x % kSlabCols, row = threadIdx.x / kSlabCols;
   const int col = ((int)blockIdx.x - ss.first[k]) * kSlabCols + cl;
   const size_t stride = sg.stride ? sg.stride : sg.P;
+  // srcnn_train_step: the finishing lanes load their parameter, momentum and
+  // gradient before the slab loads, so the update waits on no fresh load
+  const bool upd = k < ss.up.nseg && row == 0 && col < sg.P;
+  const uint32_t ui = upd ? (uint32_t)(sg.dst - ss.up.G) + col : 0;
+  float uw = 0.0f, um = 0.0f, ug = 0.0f;
+  if (upd) {
+    uw = ss.up.P[ui];
+    um = ss.up.M[ui];
+    ug = ss.up.G[ui];
+  }
   float acc = 0.0f;
   if (col < sg.P) {
     // 8 loads in flight per thread, summed in slab order
@@ -834,12 +845,26 @@ __global__ __launch_bounds__(1024) void slab_reduce_kernel(SlabSegs ss) {
     float t = 0.0f;
 #pragma unroll 8
     for (int r = 0; r < kSlabRows; r++) t += part[r][cl];
-    sg.dst[col] += t;
+    if (upd) {
+      // this element's gradient is complete, so its SGD step runs here (the
+      // same arithmetic as update_all_kernel)
+      const SlabUpdate& u = ss.up;
+      int seg = 0;
+#pragma unroll
+      for (int j = 1; j < 6; j++) seg += ui >= u.off[j];
+      sgd_step(uw, um, seg, ug + t, u.lr[seg >> 1], u.mu, u.wd, u.batch);
+      u.P[ui] = uw;
+      u.M[ui] = um;
+      u.G[ui] = 0.0f;
+    } else {
+      sg.dst[col] += t;
+    }
   }
 }
 
-int reduce_slabs(const SlabSeg* segs, int nseg, hipStream_t s) {
+int reduce_slabs(const SlabSeg* segs, int nseg, hipStream_t s, const SlabUpdate* up) {
   SlabSegs ss{};
+  if (up) ss.up = *up;
   int blocks = 0;
   for (int k = 0; k < kMaxSlabSegs; k++) {
     ss.first[k] = blocks;
@@ -889,7 +914,7 @@ template <int N1, int N2, int F1, int F3>
 static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t batch,
                const float* params, float* grads, float* sq_err, float* A1, float* A2, float* D2,
                float* A3, float* D3, float* slab, size_t slab_bytes, hipStream_t s, bool query_only,
-               size_t* need) {
+               size_t* need, const SlabUpdate* up) {
   using NetT = Net<N1, N2, F1, F3>;
   const int ow = w - F1 + 1, oh = h - F1 + 1;
   const int w3 = ow - F3 + 1, h3 = oh - F3 + 1;
@@ -973,8 +998,15 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
     const SlabSeg segs[3] = {{slab12, grads, gd, NetT::P12, 0},
                              {slab3, grads + NetT::P12, g3, NetT::P3, 0},
                              {sqs, sq_err, g3, 1, 0}};
-    int rc = l3_fused ? reduce_slabs(segs, sq_err ? 3 : 2, s) : reduce_slabs(segs, 1, s);
+    // with `up`, segments 0 and 1 are every parameter: the update rides along
+    SlabUpdate u{};
+    if (up && l3_fused) {
+      u = *up;
+      u.nseg = 2;
+    }
+    int rc = l3_fused ? reduce_slabs(segs, sq_err ? 3 : 2, s, &u) : reduce_slabs(segs, 1, s);
     if (rc) return rc;
+    if (up && l3_fused) return 2;
   }
   return 1;
 }
@@ -984,12 +1016,12 @@ static int dispatch_one(const srcnn_net* net, const float* X, const float* T, ui
                         uint32_t h, uint32_t batch, const float* params, float* grads,
                         float* sq_err, float* A1, float* A2, float* D2, float* A3, float* D3,
                         float* slab, size_t slab_bytes, hipStream_t s, bool query_only,
-                        size_t* need) {
+                        size_t* need, const SlabUpdate* up) {
   if (net->n1 != (uint32_t)N1 || net->n2 != (uint32_t)N2 || net->f1 != (uint32_t)F1 ||
       net->f2 != 1 || net->f3 != (uint32_t)F3)
     return 0;
   return run<N1, N2, F1, F3>(X, T, w, h, batch, params, grads, sq_err, A1, A2, D2, A3, D3, slab,
-                             slab_bytes, s, query_only, need);
+                             slab_bytes, s, query_only, need, up);
 }
 
 template <int N1, int N2, int F1, int F3>
@@ -1022,11 +1054,11 @@ int train_clock(int slot, double* ghz) {
 int train_fwd_bwd(const srcnn_net* net, const float* X, const float* T, uint32_t w, uint32_t h,
                   uint32_t batch, const float* params, float* grads, float* sq_err, float* A1,
                   float* A2, float* D2, float* A3, float* D3, float* slab, size_t slab_bytes,
-                  hipStream_t s, bool query_only, size_t* need) {
+                  hipStream_t s, bool query_only, size_t* need, const SlabUpdate* up) {
   int rc;
 #define SRCNN_FUSED_CASE(n1, n2, f1, f3)                                                         \
   if ((rc = dispatch_one<n1, n2, f1, f3>(net, X, T, w, h, batch, params, grads, sq_err, A1, A2,  \
-                                         D2, A3, D3, slab, slab_bytes, s, query_only, need)) != 0) \
+                                         D2, A3, D3, slab, slab_bytes, s, query_only, need, up)) != 0) \
     return rc;
   SRCNN_FUSED_CASE(64, 32, 9, 5)  // reference default (BASELINE.json configs[1])
   SRCNN_FUSED_CASE(32, 16, 9, 5)  // example_config.json

@@ -83,6 +83,8 @@ SIGNATURES = {
     "srcnn_train_workspace_bytes": (_S, [_NP, _U, _U, _U]),
     "srcnn_train_fwd_bwd": (_I, [_NP, _P, _P, _U, _U, _U, _P, _P, _P, _P, _S, _P]),
     "srcnn_update_all": (_I, [_NP, _P, _P, _P, _F, _F, ctypes.POINTER(_F), _U, _P]),
+    "srcnn_train_step": (_I, [_NP, _P, _P, _U, _U, _U, _P, _P, _P, _F, _F, ctypes.POINTER(_F), _U,
+                              _P, _P, _S, _P]),
     "srcnn_preload": (_I, [_NP]),
     "srcnn_forward_workspace_bytes": (_S, [_NP, _U, _U, _U]),
     "srcnn_forward": (_I, [_NP, _P, _U, _U, _U, _P, _P, _P, _S, _P]),
@@ -316,6 +318,16 @@ def update_all(net, params, grads, mom, momentum, wd, lr, batch, s=None):
     lr_arr = (_F * 3)(*lr)
     _call("srcnn_update_all", ctypes.byref(net), ptr(params), ptr(grads), ptr(mom), momentum, wd,
           lr_arr, batch, s)
+
+
+def train_step(net, X, T, w, h, batch, params, grads, mom, momentum, wd, lr, update_batch,
+               sq_err_dev, ws, ws_bytes, s=None):
+    """srcnn_train_step: train_fwd_bwd + update_all on one device (the update
+    fused into the gradient reduction on the fused path)."""
+    lr_arr = (_F * 3)(*lr)
+    _call("srcnn_train_step", ctypes.byref(net), ptr(X), ptr(T), w, h, batch, ptr(params),
+          ptr(grads), ptr(mom), momentum, wd, lr_arr, update_batch, ptr(sq_err_dev), ptr(ws),
+          ws_bytes, s)
 
 
 def forward_workspace_bytes(net, w, h, batch):

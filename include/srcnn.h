@@ -243,6 +243,21 @@ SRCNN_API int srcnn_get_path(void);
  *   ""        nothing launched yet on this thread */
 SRCNN_API const char* srcnn_last_path(void);
 
+/* One training step on one device: srcnn_train_fwd_bwd over the batch, then
+ * srcnn_update_all(update_batch) -- src/Main_cl.cpp:161-175 (execute_batch
+ * over the training samples, then update_parameters) with the whole batch in
+ * one chunk.  Same results as those two calls; on the fused path (nets with
+ * f2 == 1 whose tiles fit l3_delta) the update runs inside the gradient
+ * reduction, saving one launch.  Single device only: data-parallel training
+ * calls srcnn_train_fwd_bwd, srcnn_allreduce_grads, srcnn_update_all. */
+SRCNN_API int srcnn_train_step(const srcnn_net* net, const float* X,
+                               const float* T, uint32_t w, uint32_t h,
+                               uint32_t batch, float* params, float* grads,
+                               float* momentum_bufs, float momentum, float wd,
+                               const float* lr, uint32_t update_batch,
+                               float* sq_err, void* ws, size_t ws_bytes,
+                               srcnn_stream_t stream);
+
 /* ---- multi-GPU: the RCCL gradient-reduction stage ----
  * The reference has one OpenCL queue and no multi-device path
  * (src/Main_cl.cpp:157-195 runs execute_batch over the whole training set,

@@ -442,6 +442,55 @@ def test_train_step_vs_oracle(S, path, name, batch, size):
     assert not H(g_ref_dev).any()
 
 
+@pytest.mark.parametrize("name,batch,size,fused_update", [
+    ("default", 16, 33, True), ("default", 513, 33, True), ("default", 4096, 33, True),
+    ("example", 7, 33, True), ("default_f3", 7, 33, True),
+    # layer 3 on the op-level kernels / other families: update_all afterwards
+    ("default", 9, 36, False), ("wide", 3, 33, False), ("tiny", 5, 15, False)])
+def test_train_step_matches_fwd_bwd_then_update(S, path, name, batch, size, fused_update):
+    """srcnn_train_step (the update fused into the slab reduction on the fused
+    path) gives bit-identical parameters, momenta, zeroed gradients and
+    squared error to srcnn_train_fwd_bwd followed by srcnn_update_all
+    (src/Main_cl.cpp:161-175 with the batch in one chunk)."""
+    cfg = NETS[name]
+    net = S.Net(*cfg)
+    rng = np.random.default_rng(11)
+    X, T = make_batch(rng, batch, size, size)
+    params = make_params(rng, cfg, sd=0.05)
+    P = params.size
+    g0 = (1e-3 * rng.standard_normal(P)).astype(np.float32)  # accumulated earlier chunks
+    m0 = (1e-3 * rng.standard_normal(P)).astype(np.float32)
+    lr = [1e-4, 2e-4, 1e-5]
+    nbytes = S.train_workspace_bytes(net, size, size, batch)
+    ws = torch.empty(nbytes // 4 + 64, dtype=torch.float32, device="cuda")
+    Xd, Td = D(X), D(T)
+    outs = []
+    for fused in (False, True):
+        p, g, m, err = D(params), D(g0), D(m0), zeros(1)
+        if fused:
+            S.train_step(net, Xd, Td, size, size, batch, p, g, m, 0.9, 1e-3, lr, 3 * batch, err, ws,
+                         nbytes)
+        else:
+            S.train_fwd_bwd(net, Xd, Td, size, size, batch, p, g, err, ws, nbytes)
+            S.update_all(net, p, g, m, 0.9, 1e-3, lr, 3 * batch)
+        assert S.last_path() in expected_train_path(name, size, path), S.last_path()
+        outs.append([H(p), H(g), H(m), H(err)])
+    for a, b, what in zip(outs[0], outs[1], ["params", "grads", "momentum", "sq_err"]):
+        np.testing.assert_array_equal(b, a, err_msg=what)
+    assert not outs[1][1].any()
+    assert (outs[1][0] != params).mean() > 0.9  # the step moved the parameters
+    if path == 0 and fused_update:
+        # the fused path launches no separate update kernel
+        S.profile_enable(True)
+        S.profile_reset()
+        S.train_step(net, Xd, Td, size, size, batch, D(params), D(g0), D(m0), 0.9, 1e-3, lr, batch,
+                     None, ws, nbytes)
+        torch.cuda.synchronize()
+        S.profile_enable(False)
+        names = set(S.profile_stats())
+        assert "update_all" not in names and "slab_reduce" in names, names
+
+
 @pytest.mark.parametrize("w,h,batch", [(35, 31, 7), (29, 38, 5), (33, 17, 9)])
 def test_train_step_nonsquare_tiles(S, w, h, batch):
     """Non-square training tiles through the fused kernels (l12, l3 / op-level
