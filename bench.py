@@ -669,6 +669,9 @@ def main():
             "config": {"workload": workload, "global_batch": global_tiles, "batch_per_gpu": B,
                        "tile": "33x33", "parallelism": "dp%d" % world,
                        "kernel_path": kernel_path,
+                       "step_call": ("srcnn_train_fwd_bwd + srcnn_update_all" if world > 1 or
+                                     os.environ.get("SRCNN_BENCH_SEPARATE_UPDATE") else
+                                     "srcnn_train_step (SGD update inside the gradient reduction)"),
                        "grad_allreduce": (("srcnn_allreduce_grads (RCCL)" if comm else
                                            "torch.distributed all_reduce (%s)" % backend)
                                           if world > 1 else None)},
