@@ -802,6 +802,10 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
 #endif
 constexpr int kSlabCols = SRCNN_SLAB_COLS;
 constexpr int kSlabRows = 1024 / kSlabCols;
+#ifndef SRCNN_SLAB_INFLIGHT
+#define SRCNN_SLAB_INFLIGHT 8
+#endif
+constexpr int kSlabInflight = SRCNN_SLAB_INFLIGHT;
 struct SlabSegs {
   SlabSeg seg[kMaxSlabSegs];
   int first[kMaxSlabSegs + 1];
@@ -828,14 +832,14 @@ __global__ __launch_bounds__(1024) void slab_reduce_kernel(SlabSegs ss) {
   }
   float acc = 0.0f;
   if (col < sg.P) {
-    // 8 loads in flight per thread, summed in slab order
+    // kSlabInflight loads in flight per thread, summed in slab order
     int b = row;
-    for (; b + 7 * kSlabRows < sg.nslab; b += 8 * kSlabRows) {
-      float v[8];
+    for (; b + (kSlabInflight - 1) * kSlabRows < sg.nslab; b += kSlabInflight * kSlabRows) {
+      float v[kSlabInflight];
 #pragma unroll
-      for (int j = 0; j < 8; j++) v[j] = sg.slab[(size_t)(b + j * kSlabRows) * stride + col];
+      for (int j = 0; j < kSlabInflight; j++) v[j] = sg.slab[(size_t)(b + j * kSlabRows) * stride + col];
 #pragma unroll
-      for (int j = 0; j < 8; j++) acc += v[j];
+      for (int j = 0; j < kSlabInflight; j++) acc += v[j];
     }
     for (; b < sg.nslab; b += kSlabRows) acc += sg.slab[(size_t)b * stride + col];
   }
