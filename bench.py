@@ -422,8 +422,12 @@ def wide_training(S, steps=5, warmup=2, batch=4096):
     lr = [1e-4, 1e-4, 1e-5]
 
     def step():
-        S.train_fwd_bwd(net, Xd, Td, w, h, batch, params, grads, None, ws, nbytes, stream)
-        S.update_all(net, params, grads, mom, 0.9, 1e-3, lr, batch, stream)
+        if os.environ.get("SRCNN_BENCH_SEPARATE_UPDATE"):
+            S.train_fwd_bwd(net, Xd, Td, w, h, batch, params, grads, None, ws, nbytes, stream)
+            S.update_all(net, params, grads, mom, 0.9, 1e-3, lr, batch, stream)
+        else:  # the same step as the headline's (srcnn_train_step)
+            S.train_step(net, Xd, Td, w, h, batch, params, grads, mom, 0.9, 1e-3, lr, batch, None,
+                         ws, nbytes, stream)
 
     for _ in range(warmup):
         step()

@@ -328,7 +328,8 @@ static int train_impl(const srcnn_net* net, const float* X, const float* T, uint
     if (rc != 0) return rc < 0 ? rc : tag("fused", SRCNN_OK);
     rc = srcnn::wide::train_fwd_bwd(net, X, T, w, h, batch, params, grads, sq_err, A1, D1, A2, D2,
                                     static_cast<float*>(gws), gws_bytes, srcnn::as_stream(stream),
-                                    false, nullptr);
+                                    false, nullptr, up);
+    if (rc == 2 && updated) *updated = true;
     if (rc != 0) return rc < 0 ? rc : tag("wide", SRCNN_OK);
   }
   OpSequence seq;

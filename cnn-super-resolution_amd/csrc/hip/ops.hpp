@@ -112,7 +112,7 @@ namespace wide {
 int train_fwd_bwd(const srcnn_net* net, const float* X, const float* T, uint32_t w, uint32_t h,
                   uint32_t batch, const float* params, float* grads, float* sq_err, float* A1,
                   float* D1, float* A2, float* D2, float* slab, size_t slab_bytes, hipStream_t s,
-                  bool query_only, size_t* need);
+                  bool query_only, size_t* need, const fused::SlabUpdate* up = nullptr);
 int preload(const srcnn_net* net);
 // op-level launchers of the 5x5 128 <-> 64 middle layer (same contract as
 // the fast::try_* functions: 1 handled, 0 not this shape, < 0 error)

@@ -854,7 +854,7 @@ template <int N1, int N2, int F1, int F2, int F3>
 static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t batch,
                const float* params, float* grads, float* sq_err, float* A1, float* D1, float* A2,
                float* D2, float* slab, size_t slab_bytes, hipStream_t s, bool query_only,
-               size_t* need) {
+               size_t* need, const fused::SlabUpdate* up) {
   using NetT = Net<N1, N2, F1, F2, F3>;
   WGeom g;
   g.w = (int)w;
@@ -973,9 +973,15 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
                                     {slab2, grads + NetT::P1, g2.groups, NetT::P2},
                                     {slab3, grads + NetT::P1 + NetT::P2, G3, NetT::P3},
                                     {sqs, sq_err, G3, 1}};
-    if (int rc = fused::reduce_slabs(segs, sq_err ? 4 : 3, s)) return rc;
+    // with `up` (srcnn_train_step), segments 0-2 are every parameter
+    fused::SlabUpdate u{};
+    if (up) {
+      u = *up;
+      u.nseg = 3;
+    }
+    if (int rc = fused::reduce_slabs(segs, sq_err ? 4 : 3, s, &u)) return rc;
   }
-  return 1;
+  return up ? 2 : 1;
 }
 
 // ---------------------------------------------------------------------------
@@ -1144,10 +1150,10 @@ int preload(const srcnn_net* net) {
 int train_fwd_bwd(const srcnn_net* net, const float* X, const float* T, uint32_t w, uint32_t h,
                   uint32_t batch, const float* params, float* grads, float* sq_err, float* A1,
                   float* D1, float* A2, float* D2, float* slab, size_t slab_bytes, hipStream_t s,
-                  bool query_only, size_t* need) {
+                  bool query_only, size_t* need, const fused::SlabUpdate* up) {
   if (net->n1 == 128 && net->n2 == 64 && net->f1 == 9 && net->f2 == 5 && net->f3 == 5)
     return run<128, 64, 9, 5, 5>(X, T, w, h, batch, params, grads, sq_err, A1, D1, A2, D2, slab,
-                                 slab_bytes, s, query_only, need);
+                                 slab_bytes, s, query_only, need, up);
   return 0;
 }
 

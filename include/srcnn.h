@@ -247,8 +247,8 @@ SRCNN_API const char* srcnn_last_path(void);
  * srcnn_update_all(update_batch) -- src/Main_cl.cpp:161-175 (execute_batch
  * over the training samples, then update_parameters) with the whole batch in
  * one chunk.  Same results as those two calls; on the fused path (nets with
- * f2 == 1 whose tiles fit l3_delta) the update runs inside the gradient
- * reduction, saving one launch.  Single device only: data-parallel training
+ * f2 == 1 whose tiles fit l3_delta) and the wide path the update runs inside
+ * the gradient reduction, saving one launch.  Single device only: data-parallel training
  * calls srcnn_train_fwd_bwd, srcnn_allreduce_grads, srcnn_update_all. */
 SRCNN_API int srcnn_train_step(const srcnn_net* net, const float* X,
                                const float* T, uint32_t w, uint32_t h,

@@ -445,8 +445,8 @@ def test_train_step_vs_oracle(S, path, name, batch, size):
 @pytest.mark.parametrize("name,batch,size,fused_update", [
     ("default", 16, 33, True), ("default", 513, 33, True), ("default", 4096, 33, True),
     ("example", 7, 33, True), ("default_f3", 7, 33, True),
-    # layer 3 on the op-level kernels / other families: update_all afterwards
-    ("default", 9, 36, False), ("wide", 3, 33, False), ("tiny", 5, 15, False)])
+    # layer 3 on the op-level kernels / generic kernels: update_all afterwards
+    ("wide", 3, 33, True), ("default", 9, 36, False), ("tiny", 5, 15, False)])
 def test_train_step_matches_fwd_bwd_then_update(S, path, name, batch, size, fused_update):
     """srcnn_train_step (the update fused into the slab reduction on the fused
     path) gives bit-identical parameters, momenta, zeroed gradients and
