@@ -44,7 +44,7 @@
 #endif
 constexpr int kD1cTeams = SRCNN_D1C_TEAMS;
 // diagnostics builds only (results invalid): 1 no chunk barrier, 2 no chunk
-// operand DMA, 4 gW1 A operands from a register (no X gathers), 8 no relu' reads
+// operand DMA, 4 gW1 A operands from a register (no X gathers), 8 no relu' reads, 16 no slab write
 #ifdef SRCNN_D1C_DIAG
 constexpr int kD1cDiag = SRCNN_D1C_DIAG;
 #else
@@ -320,7 +320,9 @@ __global__ __launch_bounds__(256 * kD1cTeams, SRCNN_D1C_OCC) void d1c_grad12_ker
   // Row 4 lg + i of tile m is the A-operand lane lq' = 4 lg + i, i.e. tap
   // (dy0 + lg, dx0 + i) for tiles 0-3.
   float* out = slab + (size_t)blockIdx.x * P12;
-  const bool writer = team == 0;  // (two teams: team 0 holds the sums)
+  // (two teams: team 0 holds the sums; diagnostic 16: a runtime-false writer,
+  // so the accumulators stay live)
+  const bool writer = team == 0 && ((kD1cDiag & 16) ? g.batch < 0 : true);
   if (writer)
 #pragma unroll
   for (int m = 0; m < 4; m++)
