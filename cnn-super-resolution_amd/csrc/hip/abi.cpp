@@ -279,10 +279,34 @@ size_t srcnn_train_workspace_bytes(const srcnn_net* net, uint32_t w, uint32_t h,
   size_t wide_need = 0;
   if (fast_enabled() &&
       srcnn::wide::train_fwd_bwd(net, nullptr, nullptr, w, h, batch, nullptr, nullptr, nullptr,
-                                 nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr, true,
-                                 &wide_need) == 1)
+                                 nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr,
+                                 true, &wide_need) == 1)
     g = std::max(g, wide_need);
   return b + align_up(g);
+}
+
+// regions of the training workspace (srcnn_train_workspace_bytes): A1 (whole
+// 32-pixel chunks per sample) | D1 | A2 | D2 | A3 | D3 | gradient scratch
+struct TrainWs {
+  float *A1, *D1, *A2, *D2, *A3, *D3;
+  void* gws;
+};
+static TrainWs train_ws(const NetDims& d, uint32_t batch, void* ws) {
+  TrainWs L;
+  char* p = static_cast<char*>(ws);
+  auto take = [&](size_t floats) {
+    float* r = reinterpret_cast<float*>(p);
+    p += align_up(floats * batch * sizeof(float));
+    return r;
+  };
+  L.A1 = take(d.s1p);
+  L.D1 = take(d.s1);
+  L.A2 = take(d.s2);
+  L.D2 = take(d.s2);
+  L.A3 = take(d.s3);
+  L.D3 = take(d.s3);
+  L.gws = p;
+  return L;
 }
 
 // srcnn_train_fwd_bwd, and with `up` srcnn_train_step's fused variant:
@@ -300,21 +324,10 @@ static int train_impl(const srcnn_net* net, const float* X, const float* T, uint
     return fail(SRCNN_ERR_WORKSPACE, "train_fwd_bwd: workspace %zu B < %zu B", ws_bytes, need);
   size_t off[6];
   srcnn_net_offsets(net, off);
-  char* p = static_cast<char*>(ws);
-  float* A1 = reinterpret_cast<float*>(p);
-  p += align_up(d.s1p * batch * sizeof(float));
-  float* D1 = reinterpret_cast<float*>(p);
-  p += align_up(d.s1 * batch * sizeof(float));
-  float* A2 = reinterpret_cast<float*>(p);
-  p += align_up(d.s2 * batch * sizeof(float));
-  float* D2 = reinterpret_cast<float*>(p);
-  p += align_up(d.s2 * batch * sizeof(float));
-  float* A3 = reinterpret_cast<float*>(p);
-  p += align_up(d.s3 * batch * sizeof(float));
-  float* D3 = reinterpret_cast<float*>(p);
-  p += align_up(d.s3 * batch * sizeof(float));
-  void* gws = p;
-  const size_t gws_bytes = ws_bytes - (size_t)(p - static_cast<char*>(ws));
+  const TrainWs L = train_ws(d, batch, ws);
+  float *A1 = L.A1, *D1 = L.D1, *A2 = L.A2, *D2 = L.D2, *A3 = L.A3, *D3 = L.D3;
+  void* gws = L.gws;
+  const size_t gws_bytes = ws_bytes - (size_t)(static_cast<char*>(gws) - static_cast<char*>(ws));
   const float *W1 = params + off[0], *B1 = params + off[1], *W2 = params + off[2],
               *B2 = params + off[3], *W3 = params + off[4], *B3 = params + off[5];
   float *gW1 = grads + off[0], *gB1 = grads + off[1], *gW2 = grads + off[2],
@@ -327,8 +340,8 @@ static int train_impl(const srcnn_net* net, const float* X, const float* T, uint
     if (rc == 2 && updated) *updated = true;
     if (rc != 0) return rc < 0 ? rc : tag("fused", SRCNN_OK);
     rc = srcnn::wide::train_fwd_bwd(net, X, T, w, h, batch, params, grads, sq_err, A1, D1, A2, D2,
-                                    static_cast<float*>(gws), gws_bytes, srcnn::as_stream(stream),
-                                    false, nullptr, up);
+                                    A3, static_cast<float*>(gws), gws_bytes,
+                                    srcnn::as_stream(stream), false, nullptr, up);
     if (rc == 2 && updated) *updated = true;
     if (rc != 0) return rc < 0 ? rc : tag("wide", SRCNN_OK);
   }
@@ -371,6 +384,7 @@ int srcnn_train_step(const srcnn_net* net, const float* X, const float* T, uint3
                      float momentum, float wd, const float* lr, uint32_t update_batch,
                      float* sq_err, void* ws, size_t ws_bytes, srcnn_stream_t stream) {
   SRCNN_REQUIRE(net && params && grads && momentum_bufs && lr, "train_step: null argument");
+  SRCNN_REQUIRE(update_batch > 0, "train_step: update batch size must be > 0");
   size_t off[6];
   if (int rc = srcnn_net_offsets(net, off)) return rc;
   const size_t total = off[5] + 1;
@@ -393,10 +407,38 @@ int srcnn_train_step(const srcnn_net* net, const float* X, const float* T, uint3
   return srcnn_update_all(net, params, grads, momentum_bufs, momentum, wd, lr, update_batch, stream);
 }
 
+int srcnn_train_activations(const srcnn_net* net, uint32_t w, uint32_t h, uint32_t batch,
+                            const void* ws, size_t ws_bytes, float* A1, float* A2, float* A3,
+                            srcnn_stream_t stream) {
+  NetDims d;
+  if (int rc = net_dims(net, w, h, &d)) return rc;
+  if (batch == 0) return SRCNN_OK;
+  SRCNN_REQUIRE(ws && A1 && A2 && A3, "train_activations: null buffer");
+  const size_t need = srcnn_train_workspace_bytes(net, w, h, batch);
+  if (ws_bytes < need)
+    return fail(SRCNN_ERR_WORKSPACE, "train_activations: workspace %zu B < %zu B", ws_bytes, need);
+  const TrainWs L = train_ws(d, batch, const_cast<void*>(ws));
+  hipStream_t s = as_stream(stream);
+  // the fused family (the same dispatch as train_impl) stores A1 blocked per
+  // 32-pixel chunk; the wide family and the op-level kernels in HWC
+  size_t unused = 0;
+  const bool blocked =
+      fast_enabled() && srcnn::fused::train_fwd_bwd(net, nullptr, nullptr, w, h, batch, nullptr,
+                                                    nullptr, nullptr, nullptr, nullptr, nullptr,
+                                                    nullptr, nullptr, nullptr, 0, nullptr, true,
+                                                    &unused) == 1;
+  int rc = blocked ? srcnn::fused::unblock_a1(L.A1, A1, net->n1, d.w1 * d.h1, batch, s)
+                   : srcnn_memcpy_d2d(A1, L.A1, d.s1 * batch * sizeof(float), stream);
+  if (rc) return rc;
+  if ((rc = srcnn_memcpy_d2d(A2, L.A2, d.s2 * batch * sizeof(float), stream))) return rc;
+  return srcnn_memcpy_d2d(A3, L.A3, d.s3 * batch * sizeof(float), stream);
+}
+
 int srcnn_update_all(const srcnn_net* net, float* params, float* grads, float* momentum_bufs,
                      float momentum, float wd, const float* lr, uint32_t batch,
                      srcnn_stream_t stream) {
   SRCNN_REQUIRE(net && params && grads && momentum_bufs && lr, "update_all: null argument");
+  SRCNN_REQUIRE(batch > 0, "update_all: batch size must be > 0");
   size_t off[6];
   srcnn_net_offsets(net, off);
   const size_t total = off[5] + 1;

@@ -71,14 +71,28 @@ struct Scope {
 // bracket the launches that follow in this scope for the profiler
 #define SRCNN_PROFILE(name, stream) ::srcnn::prof::Scope srcnn_prof_scope_(name, stream)
 
-// Held-clock probe (MI355X_MICROARCH.md "DVFS give-back", item 6): the first
-// kClockBlocks blocks of a fused kernel record the s_memtime (shader clock)
-// and s_memrealtime (100 MHz) deltas over their lifetime into a per-kernel
-// slot of a device array; srcnn_profile_clock() reports their median ratio.
-// Two scalar counter reads per wave and one 16-B vector store per block.
+// Held-clock probe (MI355X_MICROARCH.md "DVFS give-back", item 6), built
+// only into the diagnostic variant (make PROBE=1 -> -DSRCNN_CLOCK_PROBE): the
+// first kClockBlocks blocks of a fused kernel record the s_memtime (shader
+// clock) and s_memrealtime (100 MHz) deltas over their lifetime into a
+// per-kernel slot of a device array; srcnn_profile_clock() reports their
+// median ratio.  The production kernels carry no probe.
 namespace srcnn {
 constexpr int kClockBlocks = 8;
+#ifdef SRCNN_CLOCK_PROBE
+constexpr bool kClockProbe = true;
+#else
+constexpr bool kClockProbe = false;
+#endif
 }
+#ifndef SRCNN_CLOCK_PROBE
+#define SRCNN_CLOCK_BEGIN() \
+  do {                      \
+  } while (0)
+#define SRCNN_CLOCK_END(ARR, SLOT) \
+  do {                             \
+  } while (0)
+#else
 #define SRCNN_CLOCK_BEGIN()                                                        \
   const unsigned long long srcnn_clk_c0_ = __builtin_amdgcn_s_memtime();           \
   const unsigned long long srcnn_clk_r0_ = __builtin_amdgcn_s_memrealtime()
@@ -91,6 +105,7 @@ constexpr int kClockBlocks = 8;
       (ARR)[SLOT][blockIdx.x][1] = r1_ - srcnn_clk_r0_;                            \
     }                                                                              \
   } while (0)
+#endif
 
 namespace srcnn {
 // median shader clock (GHz) over the probe blocks of one slot; -1 if unset

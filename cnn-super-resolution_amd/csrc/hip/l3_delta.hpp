@@ -126,7 +126,7 @@ template <int N2, int F3>
 __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
     const float* __restrict__ A2, const float* __restrict__ T, const float* __restrict__ W3,
     const float* __restrict__ B3, float* __restrict__ D2, float* __restrict__ slab3,
-    float* __restrict__ sq_slab, L3Geom g) {
+    float* __restrict__ sq_slab, float* __restrict__ A3out, L3Geom g) {
   // All three GEMMs run on v_mfma_f32_16x16x4_f32 over 16-pixel units, so the
   // ceil(npx2 / 16) units of a sample split evenly over the 8 waves (625
   // pixels: 40 units, 5 per wave; 32-pixel chunks would leave 4 waves a third
@@ -344,6 +344,8 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
 #pragma unroll
           for (int dx = 0; dx < F3; dx++) acc += qrow[(dy * g.w2 + dx) * K3 + dy * F3 + dx];
         const float a3 = acc + b3;
+        // A3 to the workspace (srcnn_train_activations; 1% of l3's bytes)
+        A3out[(size_t)l3_order(sample, g.batch) * nout + t] = a3;
         const float diff = a3 - tcur[k];
         const float d3 = diff * (a3 > 0.0f ? 1.0f : 0.0f);
         d3g[y * g.w2 + x + d3off] = d3;

@@ -97,6 +97,8 @@ __device__ __forceinline__ void sgd_step(float& w, float& m, int seg, float g, f
 }
 // held-clock probes (common.hpp): slot 0 l12_fwd, 1 l3_delta, 2 d1_grad12
 int train_clock(int slot, double* ghz);
+// the fused step's blocked A1 (l12_fwd_kernel) -> reference HWC [batch][npx][n1]
+int unblock_a1(const float* A1b, float* A1, uint32_t n1, uint32_t npx, uint32_t batch, hipStream_t s);
 // srcnn_preload: resolve the family's kernels for this net (1 = this family's
 // net, 0 = not, < 0 error)
 int preload(const srcnn_net* net);
@@ -111,8 +113,9 @@ int forward_clock(double* ghz);
 namespace wide {
 int train_fwd_bwd(const srcnn_net* net, const float* X, const float* T, uint32_t w, uint32_t h,
                   uint32_t batch, const float* params, float* grads, float* sq_err, float* A1,
-                  float* D1, float* A2, float* D2, float* slab, size_t slab_bytes, hipStream_t s,
-                  bool query_only, size_t* need, const fused::SlabUpdate* up = nullptr);
+                  float* D1, float* A2, float* D2, float* A3, float* slab, size_t slab_bytes,
+                  hipStream_t s, bool query_only, size_t* need,
+                  const fused::SlabUpdate* up = nullptr);
 int preload(const srcnn_net* net);
 // op-level launchers of the 5x5 128 <-> 64 middle layer (same contract as
 // the fast::try_* functions: 1 handled, 0 not this shape, < 0 error)

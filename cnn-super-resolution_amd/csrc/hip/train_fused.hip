@@ -898,7 +898,8 @@ static int grid_for_batch(uint32_t batch, int cap) { return (int)std::min<uint32
 
 template <int N2, int F3>
 static int launch_l3(const float* A2, const float* T, const float* W3, const float* B3, float* D2,
-                     float* slab3, float* sqs, const L3Geom& lg, int grid, size_t lds, hipStream_t s) {
+                     float* slab3, float* sqs, float* A3, const L3Geom& lg, int grid, size_t lds,
+                     hipStream_t s) {
   // two A2 tiles exceed the 64 KiB default dynamic LDS.  Set on every launch:
   // the attribute is per device, and one process may drive several devices
   // from several threads (cnn train --devices N)
@@ -907,7 +908,7 @@ static int launch_l3(const float* A2, const float* T, const float* W3, const flo
   if (e != hipSuccess)
     return fail(SRCNN_ERR_HIP, "hipFuncSetAttribute(l3_delta): %s", hipGetErrorString(e));
   hipLaunchKernelGGL((l3_delta_kernel<N2, F3>), dim3(grid), dim3(kL3Threads), lds, s, A2, T, W3,
-                     B3, D2, slab3, sqs, lg);
+                     B3, D2, slab3, sqs, A3, lg);
   SRCNN_LAUNCH_TRY();
   return SRCNN_OK;
 }
@@ -970,7 +971,7 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   L3Geom lg{(int)w, (int)h, ow, oh, w3, h3, (int)batch};
   if (l3_fused) {
     SRCNN_PROFILE("l3_delta_fused", s);
-    int rc = launch_l3<N2, F3>(A2, T, W3, B3, D2, slab3, sqs, lg, g3, lds3, s);
+    int rc = launch_l3<N2, F3>(A2, T, W3, B3, D2, slab3, sqs, A3, lg, g3, lds3, s);
     if (rc) return rc;
   } else {
     // ConfigBasedDataPipeline.cpp:200-323 for layer 3 on the op-level kernels
@@ -1046,6 +1047,34 @@ int preload(const srcnn_net* net) {
       (rc = preload_one<64, 32, 9, 3>(net)) || (rc = preload_one<32, 16, 9, 3>(net)))
     return rc;
   return 0;
+}
+
+// blocked A1 (l12_fwd_kernel's store layout) -> reference HWC, for
+// srcnn_train_activations: channel 32t + 8q + 4h + e of pixel 32c + li sits
+// at float 256(4t + q) + 4(li + 32h) + e of chunk c
+__global__ void unblock_a1_kernel(const float* __restrict__ A1b, float* __restrict__ A1, int n1,
+                                  int npx, size_t total) {
+  const int nch = (npx + 31) / 32;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const int ch = (int)(i % n1);
+    const size_t sp = i / n1;
+    const int p = (int)(sp % npx);
+    const size_t s = sp / npx;
+    const int c = p >> 5, li = p & 31, t = ch >> 5, r = ch & 31;
+    const int q = r >> 3, hh = (r >> 2) & 1, e = r & 3;
+    A1[i] = A1b[(s * nch + c) * (size_t)(32 * n1) + 256 * (4 * t + q) + 4 * (li + 32 * hh) + e];
+  }
+}
+
+int unblock_a1(const float* A1b, float* A1, uint32_t n1, uint32_t npx, uint32_t batch, hipStream_t s) {
+  const size_t total = (size_t)batch * npx * n1;
+  if (total == 0) return SRCNN_OK;
+  const int blocks = (int)std::min<size_t>((total + 255) / 256, 4096);
+  hipLaunchKernelGGL(unblock_a1_kernel, dim3(blocks), dim3(256), 0, s, A1b, A1, (int)n1, (int)npx,
+                     total);
+  SRCNN_LAUNCH_TRY();
+  return SRCNN_OK;
 }
 
 int train_clock(int slot, double* ghz) {

@@ -543,7 +543,8 @@ __global__ __launch_bounds__(256) void wl3_kernel(const float* __restrict__ A2,
                                                   const float* __restrict__ W3,
                                                   const float* __restrict__ B3,
                                                   float* __restrict__ D2, float* __restrict__ slab3,
-                                                  float* __restrict__ sqs, WGeom g, int qfloats) {
+                                                  float* __restrict__ sqs, float* __restrict__ A3out,
+                                                  WGeom g, int qfloats) {
   static_assert(N2 == 64 && F3 * F3 <= 32, "shape");
   constexpr int FF = F3 * F3, KP3 = (FF + 1) / 2, P3 = FF * N2 + 1;
   extern __shared__ float smem[];
@@ -620,6 +621,7 @@ __global__ __launch_bounds__(256) void wl3_kernel(const float* __restrict__ A2,
 #pragma unroll
       for (int t = 0; t < FF; t++) v += q0[((t / F3) * g.w2 + t % F3) * FF + t];
       const float a3 = v + b3;
+      A3out[(size_t)s * npx3 + o] = a3;  // to the workspace (srcnn_train_activations)
       const float diff = a3 - ts[(oy + padT) * g.w + ox + padT];
       const float d = a3 > 0.0f ? diff : 0.0f;
       sq += diff * diff;
@@ -853,7 +855,7 @@ static int set_lds(K kernel, size_t bytes) {
 template <int N1, int N2, int F1, int F2, int F3>
 static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t batch,
                const float* params, float* grads, float* sq_err, float* A1, float* D1, float* A2,
-               float* D2, float* slab, size_t slab_bytes, hipStream_t s, bool query_only,
+               float* D2, float* A3, float* slab, size_t slab_bytes, hipStream_t s, bool query_only,
                size_t* need, const fused::SlabUpdate* up) {
   using NetT = Net<N1, N2, F1, F2, F3>;
   WGeom g;
@@ -948,7 +950,7 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
     SRCNN_PROFILE("wide_l3_delta", s);
     if (int rc = set_lds(wl3_kernel<N2, F3>, lds3)) return rc;
     hipLaunchKernelGGL((wl3_kernel<N2, F3>), dim3(G3), dim3(256), lds3, s, A2, T, W3, B3, D2,
-                       slab3, sqs, g, qfloats);
+                       slab3, sqs, A3, g, qfloats);
     SRCNN_LAUNCH_TRY();
   }
   {
@@ -996,28 +998,65 @@ namespace {
 using WideNet = Net<128, 64, 9, 5, 5>;
 constexpr int kWN1 = 128, kWN2 = 64, kWF = 5;
 
-// W2 operand images of the op-level calls: one device buffer per (device,
-// stream), kept for the process (2 x 819 KB).  Calls on one stream are
-// ordered, so a stream's buffer is never in use by two calls at once.
+// W2 operand images of the op-level calls: ONE device buffer per device
+// (2 x 819 KB), reused in stream order.  A W2Image lease holds the device's
+// lock from the prepack launch to the consumer launch; a call on another
+// stream than the previous user first waits (hipStreamWaitEvent) for the
+// event recorded after that user's consumer kernel, so no two streams ever
+// share the image at once and nothing grows with the number of streams.
+struct ImgSlot {
+  float* buf = nullptr;
+  hipEvent_t done = nullptr;  // recorded after the last consumer kernel
+  hipStream_t last = nullptr;
+  bool used = false;
+  std::mutex mu;
+};
 std::mutex g_img_mu;
-std::map<std::pair<int, hipStream_t>, float*> g_img;
+std::map<int, ImgSlot> g_img;
 
-int prepacked_w2(const float* W2, float** img, hipStream_t s) {
-  int dev = 0;
-  SRCNN_HIP_TRY(hipGetDevice(&dev));
-  {
-    std::lock_guard<std::mutex> lk(g_img_mu);
-    float*& buf = g_img[{dev, s}];
-    if (!buf) SRCNN_HIP_TRY(hipMalloc(reinterpret_cast<void**>(&buf), 2 * align_f(WideNet::W2) * sizeof(float)));
-    *img = buf;
+class W2Image {
+ public:
+  // prepacks W2 into the device's image on stream s; rc() < 0 on error
+  W2Image(const float* W2, hipStream_t s) : s_(s) { rc_ = acquire(W2); }
+  ~W2Image() {
+    if (slot_) {
+      if (rc_ == SRCNN_OK) {
+        (void)hipEventRecord(slot_->done, s_);
+        slot_->last = s_;
+        slot_->used = true;
+      }
+      slot_->mu.unlock();
+    }
   }
-  SRCNN_PROFILE("wide_prepack_w2", s);
-  const int tot = 2 * WideNet::W2;
-  hipLaunchKernelGGL((prepack_w2_kernel<kWN1, kWN2, kWF>), dim3((tot + 255) / 256), dim3(256), 0, s, W2,
-                     *img, *img + align_f(WideNet::W2));
-  SRCNN_LAUNCH_TRY();
-  return SRCNN_OK;
-}
+  int rc() const { return rc_; }
+  float* img() const { return slot_ ? slot_->buf : nullptr; }
+
+ private:
+  int acquire(const float* W2) {
+    int dev = 0;
+    SRCNN_HIP_TRY(hipGetDevice(&dev));
+    {
+      std::lock_guard<std::mutex> lk(g_img_mu);
+      slot_ = &g_img[dev];  // std::map nodes never move
+    }
+    slot_->mu.lock();
+    if (!slot_->buf) {
+      SRCNN_HIP_TRY(hipMalloc(reinterpret_cast<void**>(&slot_->buf),
+                              2 * align_f(WideNet::W2) * sizeof(float)));
+      SRCNN_HIP_TRY(hipEventCreateWithFlags(&slot_->done, hipEventDisableTiming));
+    }
+    if (slot_->used && slot_->last != s_) SRCNN_HIP_TRY(hipStreamWaitEvent(s_, slot_->done, 0));
+    SRCNN_PROFILE("wide_prepack_w2", s_);
+    const int tot = 2 * WideNet::W2;
+    hipLaunchKernelGGL((prepack_w2_kernel<kWN1, kWN2, kWF>), dim3((tot + 255) / 256), dim3(256), 0,
+                       s_, W2, slot_->buf, slot_->buf + align_f(WideNet::W2));
+    SRCNN_LAUNCH_TRY();
+    return SRCNN_OK;
+  }
+  hipStream_t s_;
+  ImgSlot* slot_ = nullptr;
+  int rc_ = SRCNN_OK;
+};
 }  // namespace
 
 int op_conv_fwd(const float* in, float* out, const float* W, const float* B, uint32_t in_w,
@@ -1033,8 +1072,9 @@ int op_conv_fwd(const float* in, float* out, const float* W, const float* B, uin
     cf.img_w = std::min(ow, cf.wo) + kWF - 1;
     cf.img_h = std::min(oh, cf.wo) + kWF - 1;
   }
-  float* img = nullptr;
-  if (int rc = prepacked_w2(W, &img, s)) return rc;
+  W2Image w2i(W, s);
+  if (w2i.rc()) return w2i.rc();
+  float* img = w2i.img();
   const size_t lds = 2 * ((size_t)cf.img_w * cf.img_h * kPS + kImgSlack) * sizeof(float);
   if (int rc = set_lds(conv_mfma_kernel<kWN1, kWN2, kWF, WideNet::MT2, false, 0>, lds)) return rc;
   {
@@ -1062,8 +1102,9 @@ int op_conv_delta(const float* d_next, const float* y_curr, float* d_curr, const
     cd.img_w = std::min((int)curr_w, cd.wo) + kWF - 1;
     cd.img_h = std::min((int)curr_h, cd.wo) + kWF - 1;
   }
-  float* img = nullptr;
-  if (int rc = prepacked_w2(W_next, &img, s)) return rc;
+  W2Image w2i(W_next, s);
+  if (w2i.rc()) return w2i.rc();
+  float* img = w2i.img();
   const size_t lds = 2 * ((size_t)cd.img_w * cd.img_h * kPS + kImgSlack) * sizeof(float);
   if (int rc = set_lds(conv_mfma_kernel<kWN2, kWN1, kWF, WideNet::MT4, true, 0>, lds)) return rc;
   {
@@ -1149,10 +1190,10 @@ int preload(const srcnn_net* net) {
 
 int train_fwd_bwd(const srcnn_net* net, const float* X, const float* T, uint32_t w, uint32_t h,
                   uint32_t batch, const float* params, float* grads, float* sq_err, float* A1,
-                  float* D1, float* A2, float* D2, float* slab, size_t slab_bytes, hipStream_t s,
-                  bool query_only, size_t* need, const fused::SlabUpdate* up) {
+                  float* D1, float* A2, float* D2, float* A3, float* slab, size_t slab_bytes,
+                  hipStream_t s, bool query_only, size_t* need, const fused::SlabUpdate* up) {
   if (net->n1 == 128 && net->n2 == 64 && net->f1 == 9 && net->f2 == 5 && net->f3 == 5)
-    return run<128, 64, 9, 5, 5>(X, T, w, h, batch, params, grads, sq_err, A1, D1, A2, D2, slab,
+    return run<128, 64, 9, 5, 5>(X, T, w, h, batch, params, grads, sq_err, A1, D1, A2, D2, A3, slab,
                                  slab_bytes, s, query_only, need, up);
   return 0;
 }

@@ -4,7 +4,7 @@
 // stb_image_write (src/opencl/UtilsOpenCL.cpp load_image / write_image).
 // This is an independent codec set (PNG on the system zlib):
 //   JPEG read: baseline / extended / progressive Huffman, 8-bit, gray or
-//        YCbCr with any sampling factors (Jpeg.cpp) -- the reference's
+//        YCbCr with whole-ratio sampling factors (Jpeg.cpp) -- the reference's
 //        sample pairs and photos are JPEG (src/Main_cl.cpp:267-301)
 //   PNG  read: 8-bit gray / gray+alpha / RGB / RGBA / palette, non-interlaced;
 //        write: 8-bit gray, RGB or RGBA

@@ -9,7 +9,7 @@
 //   - baseline and extended sequential Huffman (SOF0 / SOF1) and progressive
 //     Huffman (SOF2: spectral selection and successive approximation, DC and
 //     AC, first and refinement scans, EOB runs -- T.81 G.1.2), 8-bit samples;
-//   - restart intervals (DRI / RSTn), any component sampling factors 1..4;
+//   - restart intervals (DRI / RSTn), component sampling factors 1..4 in whole ratios;
 //   - dequantisation and the 8x8 inverse DCT (T.81 A.3.3) in the published
 //     integer Loeffler-Ligtenberg-Moschytz factorisation (the IJG "islow"
 //     algorithm), rounded and clamped;
@@ -163,9 +163,10 @@ class Decoder {
   void read_adobe() {
     const size_t start = pos_;
     const int len = u16();
-    if (len < 2) bad("bad segment length");
-    if (len >= 14 && pos_ + 5 <= f_.size() && std::memcmp(&f_[pos_], "Adobe", 5) == 0)
-      adobe_transform_ = f_[start + 13];
+    if (len < 2 || start + len > f_.size()) bad("bad segment length");
+    // the transform flag is byte 11 of the payload (start + 13): the whole
+    // declared segment is inside the file, and it is long enough to hold it
+    if (len >= 14 && std::memcmp(&f_[pos_], "Adobe", 5) == 0) adobe_transform_ = f_[start + 13];
     pos_ = start + len;
   }
   void read_dqt() {
@@ -221,6 +222,10 @@ class Decoder {
       hmax_ = std::max(hmax_, c.h);
       vmax_ = std::max(vmax_, c.v);
     }
+    // upsample() maps luma column x to chroma column x / (hmax / h): only
+    // whole sampling ratios are supported (libjpeg's "fancy" ratios are not)
+    for (const auto& c : comp_)
+      if (hmax_ % c.h != 0 || vmax_ % c.v != 0) bad("unsupported (non-integral) sampling ratio");
     check_dims(width_, height_, nc);
     // every 8x8 luma block costs at least one bit of entropy-coded data (its DC
     // code), so a file much smaller than that cannot hold the image: reject it

@@ -85,6 +85,7 @@ SIGNATURES = {
     "srcnn_update_all": (_I, [_NP, _P, _P, _P, _F, _F, ctypes.POINTER(_F), _U, _P]),
     "srcnn_train_step": (_I, [_NP, _P, _P, _U, _U, _U, _P, _P, _P, _F, _F, ctypes.POINTER(_F), _U,
                               _P, _P, _S, _P]),
+    "srcnn_train_activations": (_I, [_NP, _U, _U, _U, _P, _S, _P, _P, _P, _P]),
     "srcnn_preload": (_I, [_NP]),
     "srcnn_forward_workspace_bytes": (_S, [_NP, _U, _U, _U]),
     "srcnn_forward": (_I, [_NP, _P, _U, _U, _U, _P, _P, _P, _S, _P]),
@@ -328,6 +329,13 @@ def train_step(net, X, T, w, h, batch, params, grads, mom, momentum, wd, lr, upd
     _call("srcnn_train_step", ctypes.byref(net), ptr(X), ptr(T), w, h, batch, ptr(params),
           ptr(grads), ptr(mom), momentum, wd, lr_arr, update_batch, ptr(sq_err_dev), ptr(ws),
           ws_bytes, s)
+
+
+def train_activations(net, w, h, batch, ws, ws_bytes, A1, A2, A3, s=None):
+    """srcnn_train_activations: the last training call's activations of the
+    three layers in `ws`, copied out in the reference HWC layout."""
+    _call("srcnn_train_activations", ctypes.byref(net), w, h, batch, ptr(ws), ws_bytes, ptr(A1),
+          ptr(A2), ptr(A3), s)
 
 
 def forward_workspace_bytes(net, w, h, batch):

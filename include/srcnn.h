@@ -194,7 +194,8 @@ SRCNN_API int srcnn_train_fwd_bwd(const srcnn_net* net, const float* X,
 
 /* ConfigBasedDataPipeline::update_parameters (src/ConfigBasedDataPipeline.cpp:325-361):
  * update all layers with per-layer lr[3], shared momentum / wd, then zero
- * the gradient accumulators (:353-358). */
+ * the gradient accumulators (:353-358).  batch must be > 0 (the update
+ * divides by it, update_parameters.cl:22). */
 SRCNN_API int srcnn_update_all(const srcnn_net* net, float* params,
                                float* grads, float* momentum_bufs,
                                float momentum, float wd, const float* lr,
@@ -226,8 +227,11 @@ SRCNN_API int srcnn_profile_print(void);
  * kernel ("l12_fwd_mfma", "l3_delta_fused", "delta1_grad12_fused",
  * "fwd_l123_mfma"): median over the kernel's first 8 workgroups of the
  * s_memtime / s_memrealtime (100 MHz) deltas they record in-kernel
- * (MI355X DVFS under MFMA load).  *ghz = -1 when the kernel has not run.
- * An MI355X extension; the reference has no counterpart.  Synchronous. */
+ * (MI355X DVFS under MFMA load).  *ghz = -1 when the kernel has not run,
+ * and always in the production library: the probe is compiled only into the
+ * diagnostic build (make PROBE=1, -DSRCNN_CLOCK_PROBE), so the production
+ * kernels carry no timing code.  An MI355X extension; the reference has no
+ * counterpart.  Synchronous. */
 SRCNN_API int srcnn_profile_clock(const char* kernel, double* ghz);
 
 /* Kernel-path selection (for A/B measurement and parity tests):
@@ -257,6 +261,19 @@ SRCNN_API int srcnn_train_step(const srcnn_net* net, const float* X,
                                const float* lr, uint32_t update_batch,
                                float* sq_err, void* ws, size_t ws_bytes,
                                srcnn_stream_t stream);
+
+/* Inspection seam for the parity tests (no reference counterpart; the
+ * reference's buffers are host-readable through Context::read_buffer,
+ * src/opencl/Context.cpp:235-262): the activations of the three layers (A1,
+ * A2 after ReLU; A3, the linear output) that the most recent
+ * srcnn_train_fwd_bwd / srcnn_train_step with the same net, w, h, batch and
+ * kernel path left in `ws`, copied out in the reference HWC layout:
+ * A1 [batch][h-f1+1][w-f1+1][n1], A2 [batch][..][..][n2], A3 [batch][..][..].
+ * The fused step keeps A1 blocked per 32-pixel chunk in its workspace; this
+ * undoes that.  Stream-ordered. */
+SRCNN_API int srcnn_train_activations(const srcnn_net* net, uint32_t w, uint32_t h,
+                                      uint32_t batch, const void* ws, size_t ws_bytes,
+                                      float* A1, float* A2, float* A3, srcnn_stream_t stream);
 
 /* ---- multi-GPU: the RCCL gradient-reduction stage ----
  * The reference has one OpenCL queue and no multi-device path

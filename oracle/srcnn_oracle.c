@@ -97,10 +97,12 @@ void oracle_last_delta(const float* gt, const float* y, float* d, int gt_w,
 /* ------------------------------------------------------------------ */
 /* deltas: src/kernel/layer_deltas.cl:42-127                            */
 /* ------------------------------------------------------------------ */
-void oracle_conv_delta(const float* d_next, const float* y_curr,
-                       float* d_curr, const float* W_next, int f_next,
-                       int n_curr, int n_next, int curr_w, int curr_h,
-                       int batch) {
+/* mask == NULL: relu' = [y_curr > 0] as in the reference (:72-77); else
+ * relu' = mask[same index] (the masked-oracle entry point below) */
+static void conv_delta_impl(const float* d_next, const float* y_curr,
+                            const uint8_t* mask, float* d_curr,
+                            const float* W_next, int f_next, int n_curr,
+                            int n_next, int curr_w, int curr_h, int batch) {
   const int next_w = curr_w - f_next + 1, next_h = curr_h - f_next + 1; /* :56-57 */
   /* (sample, row) pairs split over the OpenMP team, as in oracle_conv_fwd */
 #pragma omp parallel
@@ -117,7 +119,8 @@ void oracle_conv_delta(const float* d_next, const float* y_curr,
           const size_t idx = ((size_t)y * curr_w + x) * n_curr;        /* :55 */
           for (int n = 0; n < n_curr; n++) {                           /* :72-77 */
             acc[n] = 0.0f;
-            deriv[n] = yc[idx + n] > 0.0f ? 1.0f : 0.0f;
+            deriv[n] = (mask ? mask[(size_t)s * n_curr * curr_w * curr_h + idx + n] != 0
+                             : yc[idx + n] > 0.0f) ? 1.0f : 0.0f;
           }
           for (int dy = 0; dy < f_next; dy++) {                        /* :79 */
             for (int dx = 0; dx < f_next; dx++) {                      /* :80 */
@@ -144,6 +147,14 @@ void oracle_conv_delta(const float* d_next, const float* y_curr,
     free(acc);
     free(deriv);
   }
+}
+
+void oracle_conv_delta(const float* d_next, const float* y_curr,
+                       float* d_curr, const float* W_next, int f_next,
+                       int n_curr, int n_next, int curr_w, int curr_h,
+                       int batch) {
+  conv_delta_impl(d_next, y_curr, NULL, d_curr, W_next, f_next, n_curr, n_next,
+                  curr_w, curr_h, batch);
 }
 
 /* ------------------------------------------------------------------ */
@@ -347,6 +358,54 @@ void oracle_train_fwd_bwd(int n1, int n2, int f1, int f2, int f3,
   oracle_last_delta(T, A3, D3, w, h, w3, h3, batch);
   oracle_conv_delta(D3, A2, D2, params + off[4], f3, n2, 1, w2, h2, batch);
   oracle_conv_delta(D2, A1, D1, params + off[2], f2, n1, n2, w1, h1, batch);
+  oracle_conv_grad_acc(A2, D3, grads + off[4], grads + off[5], n2, 1, f3, w3, h3, batch);
+  oracle_conv_grad_acc(A1, D2, grads + off[2], grads + off[3], n1, n2, f2, w2, h2, batch);
+  oracle_conv_grad_acc(X, D1, grads + off[0], grads + off[1], 1, n1, f1, w1, h1, batch);
+  if (!acts) free(buf);
+}
+
+/* oracle_train_fwd_bwd with the ReLU decisions taken from outside:
+ * A1 = m1 ? pre1 : 0 (layer_uber_kernel.cl:88-95 with the comparison
+ * replaced), relu'(A1) = m1, likewise m2 for layer 2 (layer_deltas.cl:72-77),
+ * and m3 for the last layer's relu' quirk (last_layer_delta.cl:45).  m1 / m2 /
+ * m3 are [batch][h1][w1][n1] / [batch][h2][w2][n2] / [batch][h3][w3] bytes
+ * (0 / 1).  With the f64 build and the HIP path's own activation signs as the
+ * masks, the result is the exact gradient of the decisions the HIP path made:
+ * the parity tests use it to separate ReLU-decision flips (a pre-activation
+ * within fp32 rounding of zero) from accumulation error. */
+void oracle_train_fwd_bwd_masked(int n1, int n2, int f1, int f2, int f3,
+                                 const float* X, const float* T, int w, int h,
+                                 int batch, const float* params, float* grads,
+                                 float* acts, const uint8_t* m1,
+                                 const uint8_t* m2, const uint8_t* m3) {
+  size_t off[6];
+  layer_offsets(n1, n2, f1, f2, f3, off);
+  const int w1 = w - f1 + 1, h1 = h - f1 + 1;
+  const int w2 = w1 - f2 + 1, h2 = h1 - f2 + 1;
+  const int w3 = w2 - f3 + 1, h3 = h2 - f3 + 1;
+  const size_t s1 = (size_t)batch * w1 * h1 * n1;
+  const size_t s2 = (size_t)batch * w2 * h2 * n2;
+  const size_t s3 = (size_t)batch * w3 * h3;
+  float* buf = acts ? acts
+                    : (float*)malloc(sizeof(float) *
+                                     oracle_train_acts_floats(n1, n2, f1, f2, f3, w, h, batch));
+  float *A1 = buf, *A2 = A1 + s1, *A3 = A2 + s2, *D3 = A3 + s3, *D2 = D3 + s3,
+        *D1 = D2 + s2;
+  oracle_conv_fwd(X, A1, params + off[0], params + off[1], w, h, 1, n1, f1, 0, batch);
+  for (size_t i = 0; i < s1; i++) A1[i] = m1[i] ? A1[i] : 0.0f;
+  oracle_conv_fwd(A1, A2, params + off[2], params + off[3], w1, h1, n1, n2, f2, 0, batch);
+  for (size_t i = 0; i < s2; i++) A2[i] = m2[i] ? A2[i] : 0.0f;
+  oracle_conv_fwd(A2, A3, params + off[4], params + off[5], w2, h2, n2, 1, f3, 0, batch);
+  oracle_last_delta(T, A3, D3, w, h, w3, h3, batch);
+  for (size_t i = 0; i < s3; i++) /* last_layer_delta.cl:42-48 with relu' = m3 */
+    if (m3[i] != (A3[i] > 0.0f)) {
+      const size_t s = i / ((size_t)w3 * h3), r = i % ((size_t)w3 * h3);
+      const int pad = (w - w3) / 2;
+      const float t = T[s * (size_t)w * h + (r / w3 + pad) * (size_t)w + pad + r % w3];
+      D3[i] = m3[i] ? A3[i] - t : 0.0f;
+    }
+  conv_delta_impl(D3, A2, m2, D2, params + off[4], f3, n2, 1, w2, h2, batch);
+  conv_delta_impl(D2, A1, m1, D1, params + off[2], f2, n1, n2, w1, h1, batch);
   oracle_conv_grad_acc(A2, D3, grads + off[4], grads + off[5], n2, 1, f3, w3, h3, batch);
   oracle_conv_grad_acc(A1, D2, grads + off[2], grads + off[3], n1, n2, f2, w2, h2, batch);
   oracle_conv_grad_acc(X, D1, grads + off[0], grads + off[1], 1, n1, f1, w1, h1, batch);

@@ -94,6 +94,15 @@ void oracle_train_fwd_bwd(int n1, int n2, int f1, int f2, int f3,
                           int batch, const float* params, float* grads,
                           float* acts);
 
+/* the same chunk with the ReLU decisions of layers 1 / 2 / 3 supplied as byte
+ * masks (m1: A1's layout, m2: A2's, m3: A3's), for separating ReLU-decision flips from
+ * accumulation error in the parity tests (see srcnn_oracle.c) */
+void oracle_train_fwd_bwd_masked(int n1, int n2, int f1, int f2, int f3,
+                                 const float* X, const float* T, int w, int h,
+                                 int batch, const float* params, float* grads,
+                                 float* acts, const uint8_t* m1,
+                                 const uint8_t* m2, const uint8_t* m3);
+
 /* update all three layers, ConfigBasedDataPipeline.cpp:325-361, then zero
  * the gradient accumulators (:511-517). lr[3] per layer. */
 void oracle_update_all(int n1, int n2, int f1, int f2, int f3, float* params,

@@ -52,6 +52,7 @@ class Oracle:
                 "oracle_param_count": [i, i, i, i, i],
                 "oracle_train_acts_floats": [i, i, i, i, i, i, i, i],
                 "oracle_train_fwd_bwd": [i, i, i, i, i, fp, fp, i, i, i, fp, fp, fp],
+                "oracle_train_fwd_bwd_masked": [i, i, i, i, i, fp, fp, i, i, i, fp, fp, fp, _u8p, _u8p, _u8p],
                 "oracle_update_all": [i, i, i, i, i, fp, fp, fp, r, r, fp, u],
                 "oracle_forward": [i, i, i, i, i, fp, i, i, i, fp, fp],
             }
@@ -156,6 +157,28 @@ class Oracle:
                                    self._p(acts) if acts is not None else None)
         return grads, acts
 
+    def train_fwd_bwd_masked(self, cfg, X, T, w, h, batch, params, grads, m1, m2, m3, want_acts=False):
+        """train_fwd_bwd with the ReLU decisions of the three layers given as
+        boolean arrays in A1's / A2's / A3's layout (e.g. the HIP path's A > 0)."""
+        n1, n2, f1, f2, f3 = cfg
+        X, T, params = self.f(X), self.f(T), self.f(params)
+        grads = self.f(grads).copy()
+        m1 = np.ascontiguousarray(m1, dtype=np.uint8).ravel()
+        m2 = np.ascontiguousarray(m2, dtype=np.uint8).ravel()
+        w1, h1 = w - f1 + 1, h - f1 + 1
+        w2, h2 = w1 - f2 + 1, h1 - f2 + 1
+        m3 = np.ascontiguousarray(m3, dtype=np.uint8).ravel()
+        assert m1.size == batch * w1 * h1 * n1 and m2.size == batch * w2 * h2 * n2
+        assert m3.size == batch * (w2 - f3 + 1) * (h2 - f3 + 1)
+        acts = None
+        if want_acts:
+            acts = self.zeros(self.lib().oracle_train_acts_floats(n1, n2, f1, f2, f3, w, h, batch))
+        self.lib().oracle_train_fwd_bwd_masked(n1, n2, f1, f2, f3, self._p(X), self._p(T), w, h, batch,
+                                               self._p(params), self._p(grads),
+                                               self._p(acts) if acts is not None else None,
+                                               self._p(m1), self._p(m2), self._p(m3))
+        return grads, acts
+
     def update_all(self, cfg, params, grads, mom, momentum, wd, lr, batch):
         n1, n2, f1, f2, f3 = cfg
         params, grads, mom = self.f(params).copy(), self.f(grads).copy(), self.f(mom).copy()
@@ -185,5 +208,5 @@ def f32(a):
 
 for _name in ("set_threads", "conv_fwd", "last_delta", "conv_delta", "conv_grad_acc", "sgd_update",
               "sq_err", "buf_sum", "sub_from_all", "extract_luma", "swap_luma", "param_count",
-              "train_fwd_bwd", "update_all", "forward"):
+              "train_fwd_bwd", "train_fwd_bwd_masked", "update_all", "forward"):
     globals()[_name] = getattr(ORACLE, _name)

@@ -12,20 +12,24 @@ import numpy as np
 #   elementwise  on every SIGNIFICANT element (|exact| >= SIG x max|exact|),
 #                the relative error against the exact result -- the oracle's
 #                double-precision build (oracle/srcnn_oracle_f64.c) -- must be
-#                <= RTOL, or, where the reference's own fp32 algorithm is
-#                further off than that, no worse than K_REF x the fp32
-#                oracle's own relative error there
-# The second clause is for sums that cancel: a gradient element made of a few
-# thousand terms can come out 1000x smaller than its terms, and there any two
-# fp32 summation orders (the reference's sample-serial loop, the HIP path's
-# blocked sums) differ by far more than 1e-4 of the element.
+#                <= max(RTOL, K_REF x E), where E is the fp32 oracle's WORST
+#                relative error over the significant elements of the same
+#                array (one bound per array, not per element)
+# The K_REF x E clause is for sums that cancel: a gradient element made of a
+# few thousand terms can come out 1000x smaller than its terms, and there any
+# two fp32 summation orders (the reference's sample-serial loop, the HIP
+# path's blocked sums) differ by far more than 1e-4 of the element.  It is one
+# bound per array on purpose: which cancelling element a given order happens
+# to get right is luck, so the error one order makes at an element does not
+# bound what another order makes there; the worst error of the reference's
+# order over the array is the scale of the cancellation error it accepts.
 # Gradients add an absolute floor of FLIP_FLOOR x max|exact|: a ReLU decision
 # whose pre-activation lies within fp32 rounding of zero can go either way in
 # any fp32 order, and the whole delta of that element then enters (or leaves)
-# the weight gradients.  Measured (tools/debug/mask_flips.py, default net,
-# 600 tiles): 1 of 24M A1 elements came out +1.9e-9 where the exact value is
-# 0; its delta1 (0.2 x max|delta1|) moved gW1 by 1.2e-5 x max|gW1|, i.e. 7.8e-4
-# relative on elements near 1e-3 x max, in BOTH HIP paths (fused and generic).
+# the weight gradients.  tests/test_parity_masks_gpu.py pins this floor: it
+# recomputes the exact gradients under the HIP path's own ReLU decisions
+# (oracle_train_fwd_bwd_masked) and checks them with no floor at all, and
+# checks that every flipped decision lies inside the rounding band.
 # Measured, not assumed: tests report every error (SRCNN_PARITY_LOG).
 RTOL = 1e-4
 SIG = 1e-3
@@ -34,6 +38,13 @@ FLIP_FLOOR = 2e-5
 # SRCNN_PARITY_LOG=<file>: append one JSON line per check with the achieved
 # normwise and elementwise errors (the GPU sessions collect them)
 PARITY_LOG = os.environ.get("SRCNN_PARITY_LOG")
+
+
+def log_record(rec):
+    """Append one JSON line to the parity log (SRCNN_PARITY_LOG), if set."""
+    if PARITY_LOG:
+        with open(PARITY_LOG, "a") as fh:
+            fh.write(json.dumps(rec) + "\n")
 
 
 def dev(a, torch):
@@ -92,9 +103,7 @@ def assert_close(got, ref, rtol=RTOL, what="", ref64=None, abs_floor=0.0):
         n_over = int((over[sig] > 0).sum())
         rec.update(elementwise=el, elementwise_fp32_oracle=el_ref, significant=n_sig,
                    abs_floor=abs_floor, n_over=n_over)
-    if PARITY_LOG:
-        with open(PARITY_LOG, "a") as fh:
-            fh.write(json.dumps(rec) + "\n")
+    log_record(rec)
     assert err <= rtol, "%s: max normwise rel err %.3e > %.1e" % (what, err, rtol)
     if el is not None:
         assert n_over == 0, ("%s: %d of %d significant elements off the exact result by more than "

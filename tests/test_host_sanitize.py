@@ -45,6 +45,14 @@ def _seeds(d):
         save("rst.jpg", im, quality=80, restart_marker_blocks=2)
     except TypeError:  # older Pillow without restart markers
         pass
+    # an Adobe APP14 marker (transform byte = 1, YCbCr) right after SOI: its
+    # truncations exercise the segment-length checks of read_adobe
+    base = open(out[0], "rb").read()
+    app14 = b"\xff\xee\x00\x0eAdobe\x00\x64\x00\x00\x00\x00\x01"
+    p = os.path.join(d, "adobe.jpg")
+    with open(p, "wb") as fh:
+        fh.write(base[:2] + app14 + base[2:])
+    out.append(p)
     save("rgb.png", im)
     save("rgba.png", im.convert("RGBA"))
     save("gray.png", im.convert("L"))

@@ -676,9 +676,10 @@ def test_full_batch_gradients_vs_oracle(S):
 
 
 def test_held_clock_probe(S):
-    """srcnn_profile_clock: the in-kernel s_memtime / s_memrealtime probe of the
-    fused kernels reports a plausible shader clock after a launch (MI355X max
-    2.4 GHz; under MFMA load the chip holds less), and rejects other names."""
+    """srcnn_profile_clock: the production library carries no in-kernel probe
+    and reports -1; a diagnostic build (make PROBE=1) reports a plausible
+    shader clock after a launch (MI355X max 2.4 GHz; under MFMA load the chip
+    holds less).  Other names are rejected either way."""
     cfg = NETS["default"]
     net = S.Net(*cfg)
     batch, size = 512, 33
@@ -690,9 +691,13 @@ def test_held_clock_probe(S):
     g = zeros(params.size)
     S.train_fwd_bwd(net, D(X), D(T), size, size, batch, D(params), g, None, ws, nbytes)
     torch.cuda.synchronize()
+    probe = os.environ.get("SRCNN_EXPECT_CLOCK_PROBE") == "1"
     for k in ("l12_fwd_mfma", "l3_delta_fused", "delta1_grad12_fused"):
         ghz = S.profile_clock(k)
-        assert ghz is not None and 0.3 < ghz < 3.0, (k, ghz)
+        if probe:
+            assert ghz is not None and 0.3 < ghz < 3.0, (k, ghz)
+        else:
+            assert ghz is None, (k, ghz)
     with pytest.raises(S.SrcnnError):
         S.profile_clock("no_such_kernel")
 
