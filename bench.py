@@ -528,6 +528,9 @@ def main():
     # default; torch.distributed then only ships the RCCL id and runs the
     # barriers / max-time reduction (gloo).  --comm torch uses dist.all_reduce.
     ap.add_argument("--comm", choices=["srcnn", "torch"], default="srcnn")
+    # the timed steps replay one HIP graph of the step (srcnn_graph_*): the
+    # same kernels and collective, without a host launch per kernel
+    ap.add_argument("--graph", choices=["on", "off"], default="on")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default=None,
                     help="process-group backend (default: gloo with --comm srcnn, nccl with torch)")
     # rehearsal of the N>1 path on a single-GPU box (NOT a measurement):
@@ -547,7 +550,10 @@ def main():
     parallel.init(backend, torch.device("cuda", dev_index))
     S.set_path(0 if args.path == "auto" else 1)
     dev = torch.device("cuda", torch.cuda.current_device())
-    stream = torch.cuda.current_stream().cuda_stream
+    # the headline runs on a stream of its own (graph capture needs a created
+    # stream); the inputs are made on torch's stream, synchronised before use
+    hstream = torch.cuda.Stream(device=dev)
+    stream = hstream.cuda_stream
 
     net_t = DEFAULT_NET
     net = S.Net(*net_t)
@@ -622,6 +628,12 @@ def main():
             _mark("first warmup step enqueued")
     torch.cuda.synchronize()
     _mark("warmup done")
+    use_graph = args.graph == "on" and (world == 1 or comm is not None)
+    graph = None
+    if use_graph:
+        graph = S.Graph(step, stream)
+        graph.launch()  # one untimed replay
+        torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -632,20 +644,35 @@ def main():
     # cold).  Event pairs around every launch cost 2.5% of the step even as
     # fence-free timing events (1.011 vs 0.986 ms, same box), so the sampled
     # steps carry the instrumentation and the others run bare.
+    # With the graph, every timed step is a bare replay and the per-kernel
+    # durations come from as many profiled (non-graph) steps right after the
+    # timed region, at the same steady clock.
     every = max(1, min(args.profile_every, args.steps))
     n_prof = 0
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        on = i % every == every - 1
-        n_prof += on
-        S.profile_enable(on)
-        step()
+    if graph is not None:
+        for i in range(args.steps):
+            graph.launch()
+    else:
+        for i in range(args.steps):
+            on = i % every == every - 1
+            n_prof += on
+            S.profile_enable(on)
+            step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
     S.profile_enable(False)
     elapsed = t1 - t0
+    if graph is not None:
+        n_prof = max(1, args.steps // every)
+        S.profile_enable(True)
+        for i in range(n_prof):
+            step()
+        torch.cuda.synchronize()
+        S.profile_enable(False)
+        graph.close()
     kernel_path = S.last_path()
     if world > 1:
         e = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
@@ -706,6 +733,7 @@ def main():
             "config": {"workload": workload, "global_batch": global_tiles, "batch_per_gpu": B,
                        "tile": "33x33", "parallelism": "dp%d" % world,
                        "kernel_path": kernel_path,
+                       "hip_graph": graph is not None,
                        "step_call": ("srcnn_train_fwd_bwd + srcnn_update_all" if world > 1 or
                                      os.environ.get("SRCNN_BENCH_SEPARATE_UPDATE") else
                                      "srcnn_train_step (SGD update inside the gradient reduction)"),

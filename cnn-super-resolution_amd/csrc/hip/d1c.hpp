@@ -95,7 +95,8 @@ __global__ __launch_bounds__(256 * kD1cTeams, SRCNN_D1C_OCC) void d1c_grad12_ker
                                                             const float* __restrict__ A1,
                                                             const float* __restrict__ D2,
                                                             const float* __restrict__ W2,
-                                                            float* __restrict__ slab, Geom g, int xsf) {
+                                                            float* __restrict__ slab, Geom g, int xsf,
+                                                            int parts) {
   constexpr int N1 = 64, N2 = 32, S = kD1cS;
   static_assert(F1 == 9, "d1c: the tap tiling is for 9x9 layer-1 filters");
   constexpr int K1 = F1 * F1, NW1 = K1 * N1, NW2 = N1 * N2, P12 = NW1 + N1 + NW2 + N2;
@@ -192,27 +193,35 @@ __global__ __launch_bounds__(256 * kD1cTeams, SRCNN_D1C_OCC) void d1c_grad12_ker
     }
   };
 
+  // work items: (sample, part), `parts` consecutive chunk ranges per sample
+  // (parts > 1 only for small batches, so that every CU keeps its 4 blocks)
+  const int cpp = (nch + parts - 1) / parts;  // chunks per part
+  const int nitems = g.batch * parts;
+  auto first_chunk = [&](int it) { return (it % parts) * cpp; };
+  auto end_chunk = [&](int it) { return min(nch, (it % parts) * cpp + cpp); };
   int buf = 0, xbuf = 0;
-  if ((int)blockIdx.x < g.batch) {
-    dma_x(blockIdx.x, xsi);
-    if (team < nch) dma_chunk(blockIdx.x, team, 0);
+  if ((int)blockIdx.x < nitems) {
+    const int it0 = blockIdx.x;
+    dma_x(it0 / parts, xsi);
+    if (first_chunk(it0) + team < end_chunk(it0)) dma_chunk(it0 / parts, first_chunk(it0) + team, 0);
   }
-  for (int smp = blockIdx.x; smp < g.batch; smp += gridDim.x, xbuf ^= 1) {
-    const int next = smp + (int)gridDim.x;
+  for (int it = blockIdx.x; it < nitems; it += gridDim.x, xbuf ^= 1) {
+    const int smp = it / parts, c_beg = first_chunk(it), c_end = end_chunk(it);
+    const int nit = it + (int)gridDim.x;  // the next work item
     const float* xs = xsi + xbuf * xsf;
-    for (int cc = 0; cc < nch; cc += NT, buf ^= 1) {
-      // this chunk's operands (and at cc == 0 this sample's X tile) have
+    for (int cc = c_beg; cc < c_end; cc += NT, buf ^= 1) {
+      // this chunk's operands (and at cc == c_beg this item's X tile) have
       // landed for every wave; every wave is done with the other buffer
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (!(kD1cDiag & 1) || cc == 0) __syncthreads();
+      if (!(kD1cDiag & 1) || cc == c_beg) __syncthreads();
       const int c = cc + team;
       if (kD1cDiag & 2) {
-      } else if (c + NT < nch)
+      } else if (c + NT < c_end)
         dma_chunk(smp, c + NT, buf ^ 1);
-      else if (next < g.batch && team < nch)
-        dma_chunk(next, team, buf ^ 1);
-      if (cc == 0 && next < g.batch) dma_x(next, xsi + (xbuf ^ 1) * xsf);
-      if (c >= nch) continue;  // odd chunk count: this team idles on the last step
+      else if (nit < nitems && first_chunk(nit) + team < end_chunk(nit))
+        dma_chunk(nit / parts, first_chunk(nit) + team, buf ^ 1);
+      if (cc == c_beg && nit < nitems) dma_x(nit / parts, xsi + (xbuf ^ 1) * xsf);
+      if (c >= c_end) continue;  // odd chunk count: this team idles on the last step
       const float* d2b = d2i + buf * 1024;
       const float* a1b = a1i + (buf * 4 + wave) * 512;
 

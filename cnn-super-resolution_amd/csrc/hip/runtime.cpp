@@ -70,6 +70,10 @@ static hipEvent_t take_event() {
 }
 
 void Scope::begin(const char* name, hipStream_t s) {
+  // launches captured into a graph (srcnn_graph_begin) are not bracketed:
+  // event records inside a capture would become graph nodes
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return;
   std::lock_guard<std::mutex> lk(g_mu);
   start_ = take_event();
   stop_ = take_event();
@@ -284,6 +288,37 @@ int srcnn_event_record(srcnn_event_t ev, srcnn_stream_t stream) {
 int srcnn_event_sync(srcnn_event_t ev) {
   SRCNN_REQUIRE(ev, "srcnn_event_sync: null event");
   SRCNN_HIP_TRY(hipEventSynchronize(reinterpret_cast<hipEvent_t>(ev)));
+  return SRCNN_OK;
+}
+
+int srcnn_graph_begin(srcnn_stream_t stream) {
+  SRCNN_REQUIRE(stream, "srcnn_graph_begin: capture needs a created stream, not the NULL stream");
+  SRCNN_HIP_TRY(hipStreamBeginCapture(as_stream(stream), hipStreamCaptureModeThreadLocal));
+  return SRCNN_OK;
+}
+
+int srcnn_graph_end(srcnn_stream_t stream, srcnn_graph_t* graph) {
+  SRCNN_REQUIRE(stream && graph, "srcnn_graph_end: null argument");
+  *graph = nullptr;
+  hipGraph_t g = nullptr;
+  SRCNN_HIP_TRY(hipStreamEndCapture(as_stream(stream), &g));
+  hipGraphExec_t ex = nullptr;
+  const hipError_t e = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(g);
+  if (e != hipSuccess)
+    return srcnn::fail(SRCNN_ERR_HIP, "hipGraphInstantiate: %s", hipGetErrorString(e));
+  *graph = ex;
+  return SRCNN_OK;
+}
+
+int srcnn_graph_launch(srcnn_graph_t graph, srcnn_stream_t stream) {
+  SRCNN_REQUIRE(graph, "srcnn_graph_launch: null graph");
+  SRCNN_HIP_TRY(hipGraphLaunch(reinterpret_cast<hipGraphExec_t>(graph), as_stream(stream)));
+  return SRCNN_OK;
+}
+
+int srcnn_graph_destroy(srcnn_graph_t graph) {
+  if (graph) SRCNN_HIP_TRY(hipGraphExecDestroy(reinterpret_cast<hipGraphExec_t>(graph)));
   return SRCNN_OK;
 }
 

@@ -310,26 +310,39 @@ void ConfigBasedDataPipeline::update_parameters(LayerAllocationPool& l1, LayerAl
 
 // ---------------------------------------------------------------- data parallel
 
-void ConfigBasedDataPipeline::allreduce_gradients(GpuAllocationPool& pools, srcnn_comm_t comm) {
+void RcclExchange::allreduce(srcnn::Context& ctx, float* buf, size_t count) {
+  require(_comm != nullptr, "allreduce: null communicator");
+  check(srcnn_allreduce_grads(_comm, buf, count, ctx.stream()), "srcnn_allreduce_grads");
+}
+
+void ConfigBasedDataPipeline::allreduce_gradients(GpuAllocationPool& pools, GradientExchange& ex) {
   check_initialized(LOAD_KERNEL_BACKPROPAGATE);
-  require(comm != nullptr, "allreduce_gradients: null communicator");
   require(bind_flat(pools.layer_1, pools.layer_2, pools.layer_3),
           "allreduce_gradients needs the pipeline's own (flat) parameter buffers");
   srcnn_net nt = net();
   srcnn::Context::Launch l(*_context, *_allreduce_kernel);
-  check(srcnn_allreduce_grads(comm, _context->fptr(_flat_grads), srcnn_net_param_count(&nt),
-                              _context->stream()),
-        "allreduce_gradients");
+  ex.allreduce(*_context, _context->fptr(_flat_grads), srcnn_net_param_count(&nt));
+}
+
+void ConfigBasedDataPipeline::allreduce_gradients(GpuAllocationPool& pools, srcnn_comm_t comm) {
+  require(comm != nullptr, "allreduce_gradients: null communicator");
+  RcclExchange ex(comm);
+  allreduce_gradients(pools, ex);
+}
+
+float ConfigBasedDataPipeline::allreduce_sum(float v, GradientExchange& ex) {
+  if (_comm_scalar == gpu_nullptr) _comm_scalar = _context->allocate(srcnn::MEM_READ_WRITE, sizeof(float));
+  _context->write_buffer(_comm_scalar, &v, true);
+  ex.allreduce(*_context, _context->fptr(_comm_scalar), 1);
+  float out = 0.f;
+  _context->read_buffer(_comm_scalar, &out, true);
+  return out;
 }
 
 float ConfigBasedDataPipeline::allreduce_sum(float v, srcnn_comm_t comm) {
   require(comm != nullptr, "allreduce_sum: null communicator");
-  if (_comm_scalar == gpu_nullptr) _comm_scalar = _context->allocate(srcnn::MEM_READ_WRITE, sizeof(float));
-  _context->write_buffer(_comm_scalar, &v, true);
-  check(srcnn_allreduce_grads(comm, _context->fptr(_comm_scalar), 1, _context->stream()), "allreduce_sum");
-  float out = 0.f;
-  _context->read_buffer(_comm_scalar, &out, true);
-  return out;
+  RcclExchange ex(comm);
+  return allreduce_sum(v, ex);
 }
 
 // ---------------------------------------------------------------- parameters I/O

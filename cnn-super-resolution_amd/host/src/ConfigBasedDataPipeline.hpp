@@ -45,6 +45,25 @@ struct GpuAllocationPool {
   std::vector<SampleAllocationPool> samples;
 };
 
+/** The one exchange step of data-parallel training (an extension; the
+ * reference trains on one device): an in-place sum of `count` floats of device
+ * memory over the ranks, ordered after the work already on `ctx`'s stream. */
+class GradientExchange {
+ public:
+  virtual ~GradientExchange() = default;
+  virtual void allreduce(srcnn::Context& ctx, float* buf, size_t count) = 0;
+};
+
+/** RCCL over xGMI: srcnn_allreduce_grads on the context's stream. */
+class RcclExchange : public GradientExchange {
+ public:
+  explicit RcclExchange(srcnn_comm_t comm) : _comm(comm) {}
+  void allreduce(srcnn::Context& ctx, float* buf, size_t count) override;
+
+ private:
+  srcnn_comm_t _comm;
+};
+
 class ConfigBasedDataPipeline : public DataPipeline {
  public:
   ConfigBasedDataPipeline(Config&, srcnn::Context*);
@@ -89,13 +108,15 @@ class ConfigBasedDataPipeline : public DataPipeline {
   srcnn_net net() const;
 
   /** Data-parallel extension (the reference is single-device): sum the
-   * flat gradient buffer over the ranks of `comm` in place, on this context's
-   * stream (srcnn_allreduce_grads, RCCL over xGMI).  Call between
+   * flat gradient buffer over the ranks in place, on this context's stream
+   * (by default srcnn_allreduce_grads, RCCL over xGMI).  Call between
    * execute_batch(true, ...) on this rank's shard and update_parameters(...,
    * global training-set size).  The pools must be the pipeline's own flat
    * views (left unallocated by the caller; they are bound here if needed). */
+  void allreduce_gradients(GpuAllocationPool&, GradientExchange& ex);
   void allreduce_gradients(GpuAllocationPool&, srcnn_comm_t comm);
-  /** sum of one host float over the ranks of `comm` (blocking) */
+  /** sum of one host float over the ranks (blocking) */
+  float allreduce_sum(float value, GradientExchange& ex);
   float allreduce_sum(float value, srcnn_comm_t comm);
 
  protected:

@@ -16,16 +16,23 @@
 // of one node: one host thread per device, the epoch's training set sharded
 // contiguously over them, one RCCL all-reduce of the flat gradient buffer per
 // epoch (srcnn_allreduce_grads over ncclCommInitAll communicators), the same
-// update on every device.
+// update on every device.  Test seam: `--exchange host`
+// replaces the RCCL all-reduce by a host-side sum in rank order (ranks may
+// then share a device: `--same-device` puts every rank on --device), so the
+// sharding, the split validation sums and the exchange logic of this driver
+// run on a one-GPU machine.
 #include <dirent.h>
 #include <unistd.h>
 
 #include <algorithm>
 #include <cmath>
+#include <condition_variable>
+#include <mutex>
 #include <cstdlib>
 #include <cstring>
 #include <iostream>
 #include <map>
+#include <memory>
 #include <random>
 #include <string>
 #include <thread>
@@ -50,6 +57,8 @@ struct Args {
   int device = 0;
   int devices = 1;
   bool devices_set = false;  // --devices given: the data-parallel driver (also for N = 1)
+  bool host_exchange = false;  // --exchange host: the host-sum test seam instead of RCCL
+  bool same_device = false;    // --same-device: every rank on --device (needs --exchange host)
   size_t validation_percent = 20;  // src/Main_cl.cpp:87
   size_t mini_batches = 2;         // src/Main_cl.cpp:88
 };
@@ -70,6 +79,9 @@ void usage() {
          "  --seed N              seed of the random parameters and the epoch shuffles\n"
          "  --device D            HIP device index (default 0)\n"
          "  --devices N           train data-parallel on devices D .. D+N-1 (default 1)\n"
+         "  --exchange rccl|host  data-parallel gradient exchange (default rccl; host: a\n"
+         "                        host-side sum, a test seam)\n"
+         "  --same-device         every data-parallel rank on --device (with --exchange host)\n"
          "  --validation-percent  share of samples used for validation (default 20)\n"
          "  --mini-batches M      mini-batches per epoch (default 2)\n";
 }
@@ -92,6 +104,12 @@ bool parse(int argc, char** argv, Args& a) {
     else if (s == "--seed") { a.seed = std::stoull(value("--seed")); a.seeded = true; }
     else if (s == "--device") a.device = std::stoi(value("--device"));
     else if (s == "--devices") { a.devices = std::stoi(value("--devices")); a.devices_set = true; }
+    else if (s == "--exchange") {
+      const std::string v = value("--exchange");
+      if (v != "rccl" && v != "host") throw std::runtime_error("--exchange must be rccl or host");
+      a.host_exchange = v == "host";
+    }
+    else if (s == "--same-device") a.same_device = true;
     else if (s == "--validation-percent") a.validation_percent = std::stoul(value("--validation-percent"));
     else if (s == "--mini-batches") a.mini_batches = std::stoul(value("--mini-batches"));
     else throw std::runtime_error("unknown argument '" + s + "'");
@@ -99,6 +117,8 @@ bool parse(int argc, char** argv, Args& a) {
   if (a.help) return false;
   if (a.config.empty() || a.in.empty()) throw std::runtime_error("--config and --in are required");
   if (a.devices < 1) throw std::runtime_error("--devices must be >= 1");
+  if (a.same_device && !a.host_exchange)
+    throw std::runtime_error("--same-device needs --exchange host (RCCL takes one rank per device)");
   return true;
 }
 
@@ -167,7 +187,7 @@ std::pair<size_t, size_t> shard(size_t n, int rank, int world) {
  * all samples and draws the same epoch split (same shuffle seed), trains on
  * its shard of the training set, the gradients are all-reduced, and every
  * rank applies the update with batch = |training set|. */
-int train(ConfigBasedDataPipeline& p, const Args& a, uint64_t shuffle_seed, srcnn_comm_t comm = nullptr,
+int train(ConfigBasedDataPipeline& p, const Args& a, uint64_t shuffle_seed, GradientExchange* comm = nullptr,
           int rank = 0, int world = 1) {
   auto& ctx = *p.context();
   const bool lead = rank == 0;
@@ -216,7 +236,7 @@ int train(ConfigBasedDataPipeline& p, const Args& a, uint64_t shuffle_seed, srcn
       auto sh = shard(tr.size(), rank, world);
       std::vector<SampleAllocationPool*> mine(tr.begin() + sh.first, tr.begin() + sh.first + sh.second);
       if (!mine.empty()) p.execute_batch(true, pools, mine);
-      p.allreduce_gradients(pools, comm);
+      p.allreduce_gradients(pools, *comm);
     } else {
       p.execute_batch(true, pools, tr);
     }
@@ -227,7 +247,7 @@ int train(ConfigBasedDataPipeline& p, const Args& a, uint64_t shuffle_seed, srcn
       if (comm) {
         auto sh = shard(val.size(), rank, world);
         std::vector<SampleAllocationPool*> mine(val.begin() + sh.first, val.begin() + sh.first + sh.second);
-        err = p.allreduce_sum(mine.empty() ? 0.f : p.execute_batch(false, pools, mine), comm);
+        err = p.allreduce_sum(mine.empty() ? 0.f : p.execute_batch(false, pools, mine), *comm);
       } else {
         err = p.execute_batch(false, pools, val);
       }
@@ -251,16 +271,73 @@ int train(ConfigBasedDataPipeline& p, const Args& a, uint64_t shuffle_seed, srcn
   return error ? 1 : 0;
 }
 
+/** `--exchange host` (test seam): the ranks' buffers meet in host memory
+ * and every rank adds them up in rank order, so all ranks get bit-identical
+ * sums; two barriers per exchange (deposit, then read) keep a fast rank from
+ * overwriting its slot while a slow one still reads it. */
+class HostSumExchange {
+ public:
+  explicit HostSumExchange(int n) : _n(n), _slots(n) {}
+  class Rank : public GradientExchange {
+   public:
+    Rank(HostSumExchange* h, int r) : _h(h), _r(r) {}
+    void allreduce(srcnn::Context& ctx, float* buf, size_t count) override {
+      auto& mine = _h->_slots[_r];
+      mine.resize(count);
+      srcnn::check(srcnn_memcpy_d2h(mine.data(), buf, count * sizeof(float), ctx.stream()),
+                   "host exchange: read");
+      _h->barrier();
+      std::vector<float> sum(_h->_slots[0]);
+      for (int k = 1; k < _h->_n; ++k)
+        for (size_t i = 0; i < count; ++i) sum[i] += _h->_slots[k][i];
+      _h->barrier();
+      srcnn::check(srcnn_memcpy_h2d(buf, sum.data(), count * sizeof(float), ctx.stream()),
+                   "host exchange: write");
+    }
+
+   private:
+    HostSumExchange* _h;
+    int _r;
+  };
+
+ private:
+  void barrier() {
+    std::unique_lock<std::mutex> lk(_mu);
+    const unsigned gen = _gen;
+    if (++_arrived == _n) {
+      _arrived = 0;
+      ++_gen;
+      _cv.notify_all();
+    } else {
+      _cv.wait(lk, [&] { return _gen != gen; });
+    }
+  }
+  const int _n;
+  std::vector<std::vector<float>> _slots;
+  std::mutex _mu;
+  std::condition_variable _cv;
+  int _arrived = 0;
+  unsigned _gen = 0;
+};
+
 /** `train --devices N`: one thread per device, each with its own Context
  * (HIP device and stream) and pipeline over the same config and seed. */
 int train_data_parallel(const Config& cfg, const Args& a) {
   const int n = a.devices;
   std::vector<int> devs(n);
-  for (int i = 0; i < n; ++i) devs[i] = a.device + i;
+  for (int i = 0; i < n; ++i) devs[i] = a.same_device ? a.device : a.device + i;
   std::vector<srcnn_comm_t> comms(n, nullptr);
-  srcnn::check(srcnn_comm_init_all(comms.data(), n, devs.data()), "srcnn_comm_init_all");
-  std::cout << "Data-parallel training on " << n << " devices (" << a.device << ".."
-            << (a.device + n - 1) << "), RCCL gradient all-reduce" << std::endl;
+  std::vector<std::unique_ptr<GradientExchange>> ex(n);
+  HostSumExchange host(n);
+  if (a.host_exchange) {
+    for (int r = 0; r < n; ++r) ex[r].reset(new HostSumExchange::Rank(&host, r));
+  } else {
+    srcnn::check(srcnn_comm_init_all(comms.data(), n, devs.data()), "srcnn_comm_init_all");
+    for (int r = 0; r < n; ++r) ex[r].reset(new RcclExchange(comms[r]));
+  }
+  std::cout << "Data-parallel training on " << n << " devices (" << devs.front() << ".."
+            << devs.back() << "), " << (a.host_exchange ? "host-sum" : "RCCL") << " gradient all-reduce"
+            << std::endl;
   const uint64_t seed = a.seeded ? a.seed : std::random_device{}();
   std::vector<int> rcs(n, 0);
   std::vector<std::thread> threads;
@@ -273,7 +350,7 @@ int train_data_parallel(const Config& cfg, const Args& a) {
         ConfigBasedDataPipeline pipeline(my_cfg, &context);
         pipeline.set_random_seed(seed);  // identical initial replicas
         pipeline.init(DataPipeline::LOAD_KERNEL_ALL);
-        rcs[r] = train(pipeline, a, seed, comms[r], r, n);
+        rcs[r] = train(pipeline, a, seed, ex[r].get(), r, n);
       } catch (const std::exception& e) {
         // the other ranks may be parked in a collective this one will never
         // join: report and leave without unwinding them
@@ -284,7 +361,8 @@ int train_data_parallel(const Config& cfg, const Args& a) {
     });
   }
   for (auto& t : threads) t.join();
-  for (auto c : comms) srcnn_comm_destroy(c);
+  for (auto c : comms)
+    if (c) srcnn_comm_destroy(c);
   int rc = 0;
   for (int v : rcs) rc |= v;
   return rc;

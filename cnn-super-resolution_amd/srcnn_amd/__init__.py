@@ -65,6 +65,10 @@ SIGNATURES = {
     "srcnn_event_record": (_I, [_P, _P]),
     "srcnn_event_sync": (_I, [_P]),
     "srcnn_event_elapsed_ms": (_I, [_P, _P, ctypes.POINTER(_F)]),
+    "srcnn_graph_begin": (_I, [_P]),
+    "srcnn_graph_end": (_I, [_P, ctypes.POINTER(_P)]),
+    "srcnn_graph_launch": (_I, [_P, _P]),
+    "srcnn_graph_destroy": (_I, [_P]),
     "srcnn_conv_fwd": (_I, [_P, _P, _P, _P, _U, _U, _U, _U, _U, _I, _U, _P]),
     "srcnn_last_delta": (_I, [_P, _P, _P, _U, _U, _U, _U, _U, _P]),
     "srcnn_conv_delta": (_I, [_P, _P, _P, _P, _U, _U, _U, _U, _U, _U, _P]),
@@ -329,6 +333,36 @@ def train_step(net, X, T, w, h, batch, params, grads, mom, momentum, wd, lr, upd
     _call("srcnn_train_step", ctypes.byref(net), ptr(X), ptr(T), w, h, batch, ptr(params),
           ptr(grads), ptr(mom), momentum, wd, lr_arr, update_batch, ptr(sq_err_dev), ptr(ws),
           ws_bytes, s)
+
+
+class Graph:
+    """A replayable HIP graph of the library calls `fn()` enqueues on `stream`
+    (srcnn_graph_begin / _end); `launch()` replays it on the same stream."""
+
+    def __init__(self, fn, stream):
+        if not stream:
+            raise ValueError("graph capture needs a created stream (not the NULL stream)")
+        self.stream = stream
+        self.handle = _P()
+        _call("srcnn_graph_begin", stream)
+        try:
+            fn()
+        finally:
+            _call("srcnn_graph_end", stream, ctypes.byref(self.handle))
+
+    def launch(self):
+        _call("srcnn_graph_launch", self.handle, self.stream)
+
+    def close(self):
+        if self.handle:
+            _call("srcnn_graph_destroy", self.handle)
+            self.handle = _P()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def train_activations(net, w, h, batch, ws, ws_bytes, A1, A2, A3, s=None):

@@ -76,6 +76,21 @@ SRCNN_API int srcnn_event_record(srcnn_event_t ev, srcnn_stream_t stream);
 SRCNN_API int srcnn_event_sync(srcnn_event_t ev);
 SRCNN_API int srcnn_event_elapsed_ms(srcnn_event_t start, srcnn_event_t stop, float* ms);
 
+/* HIP graphs (an MI355X extension; the reference enqueues every kernel
+ * through clEnqueueNDRangeKernel each time, src/opencl/Kernel.cpp:85-116):
+ * the library calls enqueued on `stream` between srcnn_graph_begin and
+ * srcnn_graph_end are captured (thread-local stream capture) into one
+ * replayable graph, with their arguments frozen -- e.g. one training step
+ * (srcnn_train_step, or srcnn_train_fwd_bwd + srcnn_allreduce_grads +
+ * srcnn_update_all) launched per step by srcnn_graph_launch without a
+ * per-kernel host launch.  Profiling (srcnn_profile_enable) does not bracket
+ * captured launches.  `stream` must be a created stream, not NULL. */
+typedef void* srcnn_graph_t; /* hipGraphExec_t */
+SRCNN_API int srcnn_graph_begin(srcnn_stream_t stream);
+SRCNN_API int srcnn_graph_end(srcnn_stream_t stream, srcnn_graph_t* graph);
+SRCNN_API int srcnn_graph_launch(srcnn_graph_t graph, srcnn_stream_t stream);
+SRCNN_API int srcnn_graph_destroy(srcnn_graph_t graph);
+
 /* ---- operators: one per reference L3 launcher (src/DataPipeline.hpp:62-175) ---- */
 
 /* DataPipeline::execute_layer (src/DataPipeline.cpp:358-410) running kernel

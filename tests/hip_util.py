@@ -30,7 +30,14 @@ import numpy as np
 # recomputes the exact gradients under the HIP path's own ReLU decisions
 # (oracle_train_fwd_bwd_masked) and checks them with no floor at all, and
 # checks that every flipped decision lies inside the rounding band.
+# A third, order-independent clause applies where the caller supplies the sum
+# of the absolute values of each element's terms (mag) and their count n: an
+# element is also within tolerance if its error is at most U_ROUND x sqrt(n) x
+# mag, the probabilistic rounding-error bound of ANY fp32 summation order of
+# those terms (Higham, "Accuracy and Stability of Numerical Algorithms", 4.2 /
+# 2.8).  It only matters where a sum cancels (mag >> |exact|).
 # Measured, not assumed: tests report every error (SRCNN_PARITY_LOG).
+U_ROUND = 2.0 ** -24
 RTOL = 1e-4
 SIG = 1e-3
 K_REF = 4.0
@@ -78,11 +85,12 @@ def max_elem_rel_err(got, exact, sig=SIG):
     return float((np.abs(got[m] - exact[m]) / a[m]).max()), int(m.sum())
 
 
-def assert_close(got, ref, rtol=RTOL, what="", ref64=None, abs_floor=0.0):
+def assert_close(got, ref, rtol=RTOL, what="", ref64=None, abs_floor=0.0, mag=None, nterms=None):
     """Normwise check against the fp32 oracle `ref`; with `ref64` (the same
     computation by the double-precision oracle) also the elementwise check
     described at RTOL, each element allowed abs_floor x max|ref64| on top
-    (FLIP_FLOOR for gradients).  Returns the normwise error."""
+    (FLIP_FLOOR for gradients), and with `mag` / `nterms` the rounding-bound
+    clause described at U_ROUND.  Returns the normwise error."""
     got = np.asarray(got)
     ref = np.asarray(ref)
     assert got.shape == ref.shape, (what, got.shape, ref.shape)
@@ -98,8 +106,16 @@ def assert_close(got, ref, rtol=RTOL, what="", ref64=None, abs_floor=0.0):
         bound = max(rtol, K_REF * el_ref)
         x = np.abs(np.asarray(ref64, np.float64).ravel())
         sig = x >= SIG * x.max() if x.size and x.max() > 0 else np.zeros(x.size, bool)
-        over = np.abs(np.asarray(got, np.float64).ravel() - np.asarray(ref64, np.float64).ravel()) \
-            - bound * x - abs_floor * (x.max() if x.size else 0.0)
+        dev_ = np.abs(np.asarray(got, np.float64).ravel() - np.asarray(ref64, np.float64).ravel())
+        over = dev_ - bound * x - abs_floor * (x.max() if x.size else 0.0)
+        if mag is not None:
+            rb = U_ROUND * np.sqrt(np.asarray(nterms, np.float64)) * np.abs(np.asarray(mag, np.float64)).ravel()
+            rb = np.broadcast_to(rb, dev_.shape)
+            with np.errstate(divide="ignore", invalid="ignore"):
+                ratio = np.where(rb > 0, dev_ / rb, 0.0)
+            rec["rounding_ratio_max"] = float(ratio[sig].max()) if sig.any() else 0.0
+            rec["n_over_rtol"] = int((over[sig] > 0).sum())
+            over = np.minimum(over, dev_ - rb)
         n_over = int((over[sig] > 0).sum())
         rec.update(elementwise=el, elementwise_fp32_oracle=el_ref, significant=n_sig,
                    abs_floor=abs_floor, n_over=n_over)

@@ -167,3 +167,50 @@ def test_cli_trains_on_reference_jpeg_samples(tmp_path):
     p = cnn("-c", str(cfg2), "-i", str(src), "-o", str(out))
     assert p.returncode == 0, p.stdout
     assert Image.open(out).size == (72, 56)
+
+
+def _flat_params(path):
+    d = json.load(open(path))
+    return np.concatenate([np.asarray(d["layer%d" % i][k], np.float64) for i in (1, 2, 3)
+                           for k in ("weights", "bias")])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ranks", [2, 3])
+def test_cli_data_parallel_ranks_match_single_device(tmp_path, ranks):
+    """`train --devices N` with N > 1 on one GPU: N host threads on device 0
+    (--same-device), the gradients summed by the host-sum exchange (the test
+    seam of cnn.cpp; RCCL takes one rank per device).  This runs the driver's
+    training-set sharding (some ranks get fewer samples), the per-rank
+    validation sums and the exchange + identical update on every rank; the
+    parameters must equal the single-device run on the union of the shards up
+    to the fp32 order of the gradient sums (rank partial sums added in rank
+    order instead of one sequential sum)."""
+    samples = tmp_path / "samples"
+    subprocess.check_call([sys.executable, MAKE_SAMPLES, "--synthetic", "5", "--per-image", "4",
+                           "-o", str(samples), "-s", "33", "--seed", "4"])
+    a, b, c = tmp_path / "single.json", tmp_path / "dp.json", tmp_path / "dp1.json"
+    p = cnn(*_train_args(tmp_path, samples, a))
+    assert p.returncode == 0, p.stdout
+    single_err = [l for l in p.stdout.splitlines() if "mean validation error" in l]
+    p = cnn(*_train_args(tmp_path, samples, b, "--devices", str(ranks), "--same-device", "--exchange", "host"))
+    print(p.stdout[-2000:])
+    assert p.returncode == 0, p.stdout
+    assert "Data-parallel training on %d devices (0..0), host-sum" % ranks in p.stdout
+    dp_err = [l for l in p.stdout.splitlines() if "mean validation error" in l]
+    assert len(dp_err) == len(single_err) > 0
+    for x, y in zip(single_err, dp_err):  # "[epoch] mean validation error: v (...)"
+        vx, vy = float(x.split(":")[1].split()[0]), float(y.split(":")[1].split()[0])
+        assert vy == pytest.approx(vx, rel=1e-4)
+    ps, pd = _flat_params(a), _flat_params(b)
+    scale = np.abs(ps).max()
+    assert np.abs(pd - ps).max() <= 1e-5 * scale, np.abs(pd - ps).max() / scale
+    # one rank through the same exchange reproduces the single device exactly
+    p = cnn(*_train_args(tmp_path, samples, c, "--devices", "1", "--exchange", "host"))
+    assert p.returncode == 0, p.stdout
+    assert json.load(open(a)) == json.load(open(c))
+
+
+def test_cli_same_device_needs_host_exchange(tmp_path):
+    p = cnn("train", "-c", "x.json", "-i", str(tmp_path), "--devices", "2", "--same-device")
+    assert p.returncode == 1 and "--same-device needs --exchange host" in p.stdout

@@ -716,3 +716,59 @@ def test_invalid_arguments_raise(S):
         S.train_fwd_bwd(S.Net(64, 32, 9, 2, 5), zeros(1), zeros(1), 33, 33, 1, zeros(1), zeros(1),
                         None, zeros(1), 4)
     assert e.value.code == S.ERR_INVALID   # even f2 (Config.cpp:64-66)
+
+
+# ----------------------------------------------------------------------------
+# HIP graphs (srcnn_graph_*): a captured step replays to the same results
+# ----------------------------------------------------------------------------
+@pytest.mark.parametrize("batch", [7, 512])
+def test_graph_replay_matches_direct_steps(S, batch):
+    """Three srcnn_train_step calls and three replays of one captured
+    srcnn_train_step give bit-identical parameters, momenta and gradients; so
+    do fwd_bwd + a one-rank RCCL all-reduce + update_all (the data-parallel
+    step bench.py captures for N > 1) against the same calls made directly."""
+    cfg = NETS["default"]
+    net = S.Net(*cfg)
+    rng = np.random.default_rng(5)
+    X, T = make_batch(rng, batch, 33, 33)
+    params = make_params(rng, cfg, sd=0.05)
+    P = params.size
+    lr = [1e-4, 2e-4, 1e-5]
+    nbytes = S.train_workspace_bytes(net, 33, 33, batch)
+    ws = torch.empty(nbytes // 4 + 64, dtype=torch.float32, device="cuda")
+    st = torch.cuda.Stream()
+    sh = st.cuda_stream
+    Xd, Td = D(X), D(T)
+    comms = S.comm_init_all([0])
+    try:
+        for mode in ("train_step", "dp"):
+            outs = []
+            for use_graph in (False, True):
+                p, g, m = D(params), zeros(P), zeros(P)
+                torch.cuda.synchronize()
+
+                def step():
+                    if mode == "train_step":
+                        S.train_step(net, Xd, Td, 33, 33, batch, p, g, m, 0.9, 1e-3, lr, batch, None, ws,
+                                     nbytes, sh)
+                    else:
+                        S.train_fwd_bwd(net, Xd, Td, 33, 33, batch, p, g, None, ws, nbytes, sh)
+                        S.allreduce_grads(comms[0], g, P, sh)
+                        S.update_all(net, p, g, m, 0.9, 1e-3, lr, batch, sh)
+                if use_graph:
+                    gr = S.Graph(step, sh)
+                    for _ in range(3):
+                        gr.launch()
+                    torch.cuda.synchronize()
+                    gr.close()
+                else:
+                    for _ in range(3):
+                        step()
+                outs.append([H(p), H(g), H(m)])
+            for a, b, what in zip(outs[0], outs[1], ["params", "grads", "momentum"]):
+                np.testing.assert_array_equal(b, a, err_msg="%s %s" % (mode, what))
+            assert (outs[1][0] != params).mean() > 0.9  # the replays trained
+    finally:
+        S.comm_destroy(comms[0])
+    with pytest.raises(ValueError):
+        S.Graph(lambda: None, None)  # the NULL stream cannot be captured
