@@ -598,7 +598,7 @@ def main():
 
     # The single-GPU side lines (the wide net, one 256x256 tile, 4K inference)
     # are measured before the headline.  Order and pause matter on this part
-    # (tools/debug/first_step.py): right after ~0.15 s of the
+    # (tools/first_step.py): right after ~0.15 s of the
     # wide net's full-power load the GPU stalls the next launch for 8-24 ms
     # (a power-state transition; a 0.2 s idle pause avoids it), and a step
     # launched on an idle GPU runs through a ~25 ms clock ramp.  So: wide net,

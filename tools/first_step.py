@@ -1,7 +1,7 @@
 """Where does the first default-net step after another workload wait?
 Wall time of each call of the first steps with a device sync after it."""
 import os, sys, time
-ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 import numpy as np  # noqa: E402
