@@ -15,8 +15,10 @@
 //                          then driven by its own host thread
 // The collective is enqueued on the caller's compute stream, so it is ordered
 // after the gradient kernels and before the update without host syncs.
+#include <dlfcn.h>
 #include <rccl/rccl.h>
 
+#include <cstdio>
 #include <cstring>
 
 #include "common.hpp"
@@ -90,6 +92,21 @@ int srcnn_comm_group_start(void) {
 
 int srcnn_comm_group_end(void) {
   SRCNN_NCCL_TRY(ncclGroupEnd());
+  return SRCNN_OK;
+}
+
+int srcnn_comm_version(int* version, char* path, size_t len) {
+  if (version) SRCNN_NCCL_TRY(ncclGetVersion(version));
+  if (path && len) {
+    // the file the dynamic loader bound ncclAllReduce to (its DT_NEEDED
+    // soname librccl.so.1 resolves to whichever copy loaded first)
+    Dl_info di;
+    const void* fn = reinterpret_cast<const void*>(&ncclAllReduce);
+    if (dladdr(fn, &di) && di.dli_fname)
+      std::snprintf(path, len, "%s", di.dli_fname);
+    else
+      path[0] = 0;
+  }
   return SRCNN_OK;
 }
 

@@ -30,6 +30,7 @@
 #include <mutex>
 #include <cstdlib>
 #include <cstring>
+#include <fstream>
 #include <iostream>
 #include <map>
 #include <memory>
@@ -49,7 +50,7 @@ using namespace cnn_sr;
 namespace {
 
 struct Args {
-  bool train = false, dry = false, profile = false, help = false;
+  bool train = false, dry = false, profile = false, help = false, version = false;
   std::string config, in, out;
   size_t epochs = 0;
   uint64_t seed = 0;
@@ -69,6 +70,7 @@ void usage() {
          "           [--seed N] [--device D] [--devices N] [--validation-percent P]\n"
          "           [--mini-batches M]\n\n"
          "  -h, --help            print this help\n"
+         "  --version             library ABI, HIP runtime and RCCL the binary runs on\n"
          "  train                 train mode\n"
          "  dry                   do not store the result\n"
          "  profile               print kernel execution times\n"
@@ -94,6 +96,7 @@ bool parse(int argc, char** argv, Args& a) {
       return argv[++i];
     };
     if (s == "-h" || s == "--help" || s == "help") a.help = true;
+    else if (s == "--version") a.version = true;
     else if (s == "train") a.train = true;
     else if (s == "dry") a.dry = true;
     else if (s == "profile") a.profile = true;
@@ -114,7 +117,7 @@ bool parse(int argc, char** argv, Args& a) {
     else if (s == "--mini-batches") a.mini_batches = std::stoul(value("--mini-batches"));
     else throw std::runtime_error("unknown argument '" + s + "'");
   }
-  if (a.help) return false;
+  if (a.help || a.version) return false;
   if (a.config.empty() || a.in.empty()) throw std::runtime_error("--config and --in are required");
   if (a.devices < 1) throw std::runtime_error("--devices must be >= 1");
   if (a.same_device && !a.host_exchange)
@@ -368,12 +371,36 @@ int train_data_parallel(const Config& cfg, const Args& a) {
   return rc;
 }
 
+/** `cnn --version`: the C ABI version, the HIP runtime and the RCCL this
+ * process loaded (the RCCL matches the HIP runtime) */
+void print_version() {
+  std::cout << "libsrcnn_hip ABI " << srcnn_abi_version() << std::endl;
+  std::string hip;
+  std::ifstream maps("/proc/self/maps");
+  for (std::string line; std::getline(maps, line);) {
+    const size_t at = line.find('/');
+    if (at != std::string::npos && line.find("libamdhip64.so") != std::string::npos) {
+      hip = line.substr(at);
+      break;
+    }
+  }
+  std::cout << "HIP runtime " << (hip.empty() ? "(not loaded)" : hip) << std::endl;
+  int v = 0;
+  char path[4096] = {0};
+  srcnn::check(srcnn_comm_version(&v, path, sizeof(path)), "srcnn_comm_version");
+  std::cout << "RCCL " << v / 10000 << "." << (v / 100) % 100 << "." << v % 100 << " " << path << std::endl;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
   Args a;
   try {
     if (!parse(argc, argv, a)) {
+      if (a.version) {
+        print_version();
+        return 0;
+      }
       usage();
       return 0;
     }

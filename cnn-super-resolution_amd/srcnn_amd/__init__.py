@@ -111,6 +111,7 @@ SIGNATURES = {
     "srcnn_comm_group_start": (_I, []),
     "srcnn_comm_group_end": (_I, []),
     "srcnn_allreduce_grads": (_I, [_P, _P, _S, _P]),
+    "srcnn_comm_version": (_I, [ctypes.POINTER(_I), ctypes.c_char_p, _S]),
 }
 
 for _name, (_res, _args) in SIGNATURES.items():
@@ -435,6 +436,14 @@ def comm_rank(c):
     r, n = _I(), _I()
     _call("srcnn_comm_rank", c, ctypes.byref(r), ctypes.byref(n))
     return r.value, n.value
+
+
+def comm_version():
+    """(RCCL version code, path of the librccl the library is bound to)."""
+    v = _I()
+    buf = ctypes.create_string_buffer(4096)
+    _call("srcnn_comm_version", ctypes.byref(v), buf, len(buf))
+    return v.value, buf.value.decode()
 
 
 def allreduce_grads(c, buf, count, s=None):

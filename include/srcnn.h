@@ -312,6 +312,13 @@ SRCNN_API int srcnn_comm_rank(srcnn_comm_t comm, int* rank, int* nranks);
 /* ncclGroupStart / End: one thread issuing the collectives of several devices */
 SRCNN_API int srcnn_comm_group_start(void);
 SRCNN_API int srcnn_comm_group_end(void);
+/* RCCL the library runs on: ncclGetVersion (e.g. 22707 = 2.27.7) and the file
+ * the loader bound it to.  The library links librccl.so.1 by soname, so a
+ * process gets the RCCL of the HIP runtime it loaded first: the ROCm
+ * install's (/opt/rocm/lib) for a C++ host such as `cnn`, PyTorch's bundled
+ * copy (torch/lib) in a Python process that imported torch -- each matching
+ * its libamdhip64.so.7.  Either pointer may be NULL. */
+SRCNN_API int srcnn_comm_version(int* version, char* path, size_t len);
 /* in-place sum of `count` floats of `buf` over all ranks, enqueued on `stream`
  * (ordered after the gradient kernels, before the update; no host sync) */
 SRCNN_API int srcnn_allreduce_grads(srcnn_comm_t comm, float* buf, size_t count,

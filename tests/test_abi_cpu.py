@@ -99,3 +99,34 @@ def test_path_switch(S):
     S.set_path(0)
     with pytest.raises(S.SrcnnError):
         S.set_path(7)
+
+
+def _loaded(libname):
+    with open("/proc/self/maps") as fh:
+        for line in fh:
+            if libname in line and "/" in line:
+                return line[line.index("/"):].strip()
+    return None
+
+
+def test_rccl_matches_the_hip_runtime_in_python(S):
+    """libsrcnn_hip.so links librccl.so.1 by soname, so in a
+    Python process that imported torch first it binds PyTorch's bundled RCCL,
+    the one built for the HIP runtime (libamdhip64) torch loaded.  Both come
+    from the same directory; srcnn_comm_version reports which."""
+    version, path = S.comm_version()
+    assert version >= 22000, version
+    hip = _loaded("libamdhip64.so")
+    assert hip is not None
+    assert os.path.dirname(os.path.realpath(path)) == os.path.dirname(os.path.realpath(hip)), (path, hip)
+
+
+def test_rccl_matches_the_hip_runtime_in_cnn():
+    """The C++ host (`cnn`) loads the ROCm install's HIP runtime and RCCL."""
+    import subprocess
+    cnn = os.path.join(ROOT, "cnn-super-resolution_amd", "bin", "cnn")
+    out = subprocess.run([cnn, "--version"], capture_output=True, text=True, timeout=60).stdout
+    lines = dict(l.split(" ", 1) for l in out.splitlines() if l.startswith(("HIP", "RCCL")))
+    hip = lines["HIP"].split()[-1]
+    rccl = lines["RCCL"].split()[-1]
+    assert os.path.dirname(os.path.realpath(hip)) == os.path.dirname(os.path.realpath(rccl)), out
