@@ -24,6 +24,8 @@
 // sample -> block -> wave assignment is static and every sum has a fixed
 // order; no float atomics anywhere.
 #include <algorithm>
+#include <atomic>
+#include <cstdlib>
 #include <type_traits>
 
 #include "common.hpp"
@@ -282,9 +284,21 @@ __global__ __launch_bounds__(256, SRCNN_L12_WAVES) void l12_fwd_kernel(
 
 #include "l3_delta.hpp"
 #include "l3s.hpp"
-#ifndef SRCNN_L3S
-#define SRCNN_L3S 0  // layer 3 of the fused step: 1 = l3s_kernel (two-pass streaming), 0 = l3_delta_kernel
+// Layer 3 of the fused step: l3s_kernel (two-pass streaming, two blocks per
+// CU) for batches below SRCNN_L3S_BELOW tiles, l3_delta_kernel (the A2 tile
+// resident in LDS, one block per CU) above.  Environment SRCNN_L3S=1 / 0
+// forces one of them (A/B runs and the parity tests of both).
+#ifndef SRCNN_L3S_BELOW
+#define SRCNN_L3S_BELOW 0
 #endif
+std::atomic<int> g_l3s_force{[] {
+  const char* e = getenv("SRCNN_L3S");
+  return e && *e ? atoi(e) : -1;
+}()};
+static bool want_l3s(uint32_t batch) {
+  const int v = g_l3s_force.load(std::memory_order_relaxed);
+  return v >= 0 ? v != 0 : batch < (uint32_t)SRCNN_L3S_BELOW;
+}
 
 #ifdef SRCNN_D1_TIMING
 // diagnostics build only: wave 0's cycles per section of the chunk loop
@@ -949,7 +963,7 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   // l3s (two-pass streaming, up to kL3sMaxPx A2 pixels) where it fits, else
   // l3_delta (the A2 tile resident in LDS) where that fits
   const size_t lds3s = l3s_lds_bytes<N2, F3>(ow, oh);
-  const bool use_l3s = SRCNN_L3S && ow * oh <= kL3sMaxPx && w3 * h3 <= kL3sMaxOut && lds3s <= 160 * 1024;
+  const bool use_l3s = want_l3s(batch) && ow * oh <= kL3sMaxPx && w3 * h3 <= kL3sMaxOut && lds3s <= 160 * 1024;
   const size_t lds3 = use_l3s ? lds3s : l3_lds_bytes<N2, F3>(ow, oh);
   const bool l3_fused =
       use_l3s ||
@@ -1105,6 +1119,12 @@ int unblock_a1(const float* A1b, float* A1, uint32_t n1, uint32_t npx, uint32_t 
   hipLaunchKernelGGL(unblock_a1_kernel, dim3(blocks), dim3(256), 0, s, A1b, A1, (int)n1, (int)npx,
                      total);
   SRCNN_LAUNCH_TRY();
+  return SRCNN_OK;
+}
+
+int set_l3_kernel(int v) {
+  SRCNN_REQUIRE(v >= -1 && v <= 1, "srcnn_set_kernel_option(l3s): %d not in {-1, 0, 1}", v);
+  g_l3s_force.store(v);
   return SRCNN_OK;
 }
 
