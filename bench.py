@@ -529,8 +529,10 @@ def main():
     # barriers / max-time reduction (gloo).  --comm torch uses dist.all_reduce.
     ap.add_argument("--comm", choices=["srcnn", "torch"], default="srcnn")
     # the timed steps replay one HIP graph of the step (srcnn_graph_*): the
-    # same kernels and collective, without a host launch per kernel
-    ap.add_argument("--graph", choices=["on", "off"], default="on")
+    # same kernels and collective without a host launch per kernel.  Default:
+    # on for N > 1 (no host launch jitter between the ranks' collectives), off
+    # for N = 1, where it measured the same (0.8975 vs 0.894 ms, same box)
+    ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default=None,
                     help="process-group backend (default: gloo with --comm srcnn, nccl with torch)")
     # rehearsal of the N>1 path on a single-GPU box (NOT a measurement):
@@ -628,7 +630,7 @@ def main():
             _mark("first warmup step enqueued")
     torch.cuda.synchronize()
     _mark("warmup done")
-    use_graph = args.graph == "on" and (world == 1 or comm is not None)
+    use_graph = (args.graph == "on" or (args.graph == "auto" and world > 1)) and (world == 1 or comm is not None)
     graph = None
     if use_graph:
         try:

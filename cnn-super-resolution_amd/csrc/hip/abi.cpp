@@ -6,7 +6,6 @@
 // "auto", otherwise the shape-generic kernels of ops_generic.hip.  There is
 // no CPU fallback: every path launches HIP kernels.
 #include <algorithm>
-#include <cstring>
 
 #include "common.hpp"
 #include "ops.hpp"
@@ -86,11 +85,6 @@ extern "C" {
 
 const char* srcnn_last_path(void) { return t_path; }
 
-int srcnn_set_kernel_option(const char* name, int value) {
-  SRCNN_REQUIRE(name, "srcnn_set_kernel_option: null name");
-  if (!strcmp(name, "l3s")) return srcnn::fused::set_l3_kernel(value);
-  return fail(SRCNN_ERR_INVALID, "srcnn_set_kernel_option: unknown option '%s'", name);
-}
 
 int srcnn_fill_f32(float* dst, float value, size_t count, srcnn_stream_t stream) {
   if (count == 0) return SRCNN_OK;

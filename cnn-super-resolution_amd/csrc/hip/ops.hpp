@@ -97,8 +97,6 @@ __device__ __forceinline__ void sgd_step(float& w, float& m, int seg, float g, f
 }
 // held-clock probes (common.hpp): slot 0 l12_fwd, 1 l3_delta, 2 d1_grad12
 int train_clock(int slot, double* ghz);
-// layer-3 kernel of the fused step: -1 by batch size, 0 l3_delta, 1 l3s
-int set_l3_kernel(int v);
 // the fused step's blocked A1 (l12_fwd_kernel) -> reference HWC [batch][npx][n1]
 int unblock_a1(const float* A1b, float* A1, uint32_t n1, uint32_t npx, uint32_t batch, hipStream_t s);
 // srcnn_preload: resolve the family's kernels for this net (1 = this family's

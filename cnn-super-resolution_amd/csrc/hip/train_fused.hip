@@ -24,8 +24,6 @@
 // sample -> block -> wave assignment is static and every sum has a fixed
 // order; no float atomics anywhere.
 #include <algorithm>
-#include <atomic>
-#include <cstdlib>
 #include <type_traits>
 
 #include "common.hpp"
@@ -283,22 +281,6 @@ __global__ __launch_bounds__(256, SRCNN_L12_WAVES) void l12_fwd_kernel(
 #undef SRCNN_W1F
 
 #include "l3_delta.hpp"
-#include "l3s.hpp"
-// Layer 3 of the fused step: l3s_kernel (two-pass streaming, two blocks per
-// CU) for batches below SRCNN_L3S_BELOW tiles, l3_delta_kernel (the A2 tile
-// resident in LDS, one block per CU) above.  Environment SRCNN_L3S=1 / 0
-// forces one of them (A/B runs and the parity tests of both).
-#ifndef SRCNN_L3S_BELOW
-#define SRCNN_L3S_BELOW 0
-#endif
-std::atomic<int> g_l3s_force{[] {
-  const char* e = getenv("SRCNN_L3S");
-  return e && *e ? atoi(e) : -1;
-}()};
-static bool want_l3s(uint32_t batch) {
-  const int v = g_l3s_force.load(std::memory_order_relaxed);
-  return v >= 0 ? v != 0 : batch < (uint32_t)SRCNN_L3S_BELOW;
-}
 
 #ifdef SRCNN_D1_TIMING
 // diagnostics build only: wave 0's cycles per section of the chunk loop
@@ -931,20 +913,6 @@ static int launch_l3(const float* A2, const float* T, const float* W3, const flo
   return SRCNN_OK;
 }
 
-template <int N2, int F3>
-static int launch_l3s(const float* A2, const float* T, const float* W3, const float* B3, float* D2,
-                      float* slab3, float* sqs, float* A3, const L3Geom& lg, int grid, size_t lds,
-                      hipStream_t s) {
-  hipError_t e = hipFuncSetAttribute((const void*)l3s_kernel<N2, F3>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  if (e != hipSuccess)
-    return fail(SRCNN_ERR_HIP, "hipFuncSetAttribute(l3s): %s", hipGetErrorString(e));
-  hipLaunchKernelGGL((l3s_kernel<N2, F3>), dim3(grid), dim3(kL3sThreads), lds, s, A2, T, W3, B3, D2,
-                     slab3, sqs, A3, lg);
-  SRCNN_LAUNCH_TRY();
-  return SRCNN_OK;
-}
-
 // Returns 1 if the shape is specialised (and the step was enqueued), 0 if
 // not (caller falls back to the op-by-op path), <0 on error.
 template <int N1, int N2, int F1, int F3>
@@ -960,18 +928,12 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   // f1 = 9).  Larger tiles (e.g. the reference's 36x36 samples, profile.py:7)
   // keep l12 and d1 and run layer 3 through the op-level kernels instead
   // (ops_fast.hip: L3 forward, last delta, delta2, gW3 over HWC A2 / A3 / D3).
-  // l3s (two-pass streaming, up to kL3sMaxPx A2 pixels) where it fits, else
-  // l3_delta (the A2 tile resident in LDS) where that fits
-  const size_t lds3s = l3s_lds_bytes<N2, F3>(ow, oh);
-  const bool use_l3s = want_l3s(batch) && ow * oh <= kL3sMaxPx && w3 * h3 <= kL3sMaxOut && lds3s <= 160 * 1024;
-  const size_t lds3 = use_l3s ? lds3s : l3_lds_bytes<N2, F3>(ow, oh);
+  const size_t lds3 = l3_lds_bytes<N2, F3>(ow, oh);
   const bool l3_fused =
-      use_l3s ||
-      (lds3 <= 160 * 1024 && w3 * h3 <= kL3MaxOut &&
-       ((ow * oh + 15) / 16 + kL3Threads / 64 - 1) / (kL3Threads / 64) <= L3Lds<N2, F3>::kUnitsPerWave);
+      lds3 <= 160 * 1024 && w3 * h3 <= kL3MaxOut &&
+      ((ow * oh + 15) / 16 + kL3Threads / 64 - 1) / (kL3Threads / 64) <= L3Lds<N2, F3>::kUnitsPerWave;
   const int g12 = grid_for_batch(batch, SRCNN_L12_GRID);
-  // l3s: as many blocks as share the CUs (2 at 68 KB of LDS); l3_delta: one per CU
-  const int g3 = grid_for_batch(batch, use_l3s ? 256 * (int)std::max<size_t>(1, std::min<size_t>(2, (160 * 1024) / lds3s)) : 256);
+  const int g3 = grid_for_batch(batch, 256);
   const bool kD1c = SRCNN_D1C && N1 == 64 && N2 == 32 && F1 == 9 && d1c_fits(w, h);
   // d1c below kD1cGrid samples: each sample's chunks split into `parts`
   // ranges (work items), so the grid still fills every CU's 4 block slots
@@ -1015,8 +977,7 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   L3Geom lg{(int)w, (int)h, ow, oh, w3, h3, (int)batch};
   if (l3_fused) {
     SRCNN_PROFILE("l3_delta_fused", s);
-    int rc = use_l3s ? launch_l3s<N2, F3>(A2, T, W3, B3, D2, slab3, sqs, A3, lg, g3, lds3, s)
-                     : launch_l3<N2, F3>(A2, T, W3, B3, D2, slab3, sqs, A3, lg, g3, lds3, s);
+    int rc = launch_l3<N2, F3>(A2, T, W3, B3, D2, slab3, sqs, A3, lg, g3, lds3, s);
     if (rc) return rc;
   } else {
     // ConfigBasedDataPipeline.cpp:200-323 for layer 3 on the op-level kernels
@@ -1080,9 +1041,9 @@ static int preload_one(const srcnn_net* net) {
       net->f2 != 1 || net->f3 != (uint32_t)F3)
     return 0;
   const void* k[] = {(const void*)l12_fwd_kernel<N1, N2, F1>, (const void*)l3_delta_kernel<N2, F3>,
-                     (const void*)l3s_kernel<N2, F3>, (const void*)d1_grad12_kernel<N1, N2, F1>,
-                     (const void*)slab_reduce_kernel, (const void*)d1c_grad12_kernel<9>};
-  int rc = resolve_kernels(k, SRCNN_D1C && N1 == 64 && N2 == 32 && F1 == 9 ? 6 : 5);
+                     (const void*)d1_grad12_kernel<N1, N2, F1>, (const void*)slab_reduce_kernel,
+                     (const void*)d1c_grad12_kernel<9>};
+  int rc = resolve_kernels(k, SRCNN_D1C && N1 == 64 && N2 == 32 && F1 == 9 ? 5 : 4);
   return rc ? rc : 1;
 }
 
@@ -1119,12 +1080,6 @@ int unblock_a1(const float* A1b, float* A1, uint32_t n1, uint32_t npx, uint32_t 
   hipLaunchKernelGGL(unblock_a1_kernel, dim3(blocks), dim3(256), 0, s, A1b, A1, (int)n1, (int)npx,
                      total);
   SRCNN_LAUNCH_TRY();
-  return SRCNN_OK;
-}
-
-int set_l3_kernel(int v) {
-  SRCNN_REQUIRE(v >= -1 && v <= 1, "srcnn_set_kernel_option(l3s): %d not in {-1, 0, 1}", v);
-  g_l3s_force.store(v);
   return SRCNN_OK;
 }
 

@@ -103,7 +103,6 @@ SIGNATURES = {
     "srcnn_set_path": (_I, [_I]),
     "srcnn_get_path": (_I, []),
     "srcnn_last_path": (ctypes.c_char_p, []),
-    "srcnn_set_kernel_option": (_I, [ctypes.c_char_p, _I]),
     "srcnn_comm_id": (_I, [ctypes.c_char_p]),
     "srcnn_comm_init_rank": (_I, [ctypes.POINTER(_P), _I, ctypes.c_char_p, _I]),
     "srcnn_comm_init_all": (_I, [ctypes.POINTER(_P), _I, ctypes.POINTER(_I)]),
@@ -365,11 +364,6 @@ class Graph:
             self.close()
         except Exception:
             pass
-
-
-def set_kernel_option(name, value):
-    """srcnn_set_kernel_option: select a kernel variant (e.g. "l3s")."""
-    _call("srcnn_set_kernel_option", name.encode(), int(value))
 
 
 def train_activations(net, w, h, batch, ws, ws_bytes, A1, A2, A3, s=None):

@@ -261,12 +261,6 @@ SRCNN_API int srcnn_get_path(void);
  *   "generic" ops_generic.hip (any shape; one thread per output)
  *   ""        nothing launched yet on this thread */
 SRCNN_API const char* srcnn_last_path(void);
-/* Kernel variants inside a family (A/B measurement and parity tests):
- *   "l3s"  layer 3 of the fused step: 1 = two-pass streaming l3s kernel,
- *          0 = l3_delta (A2 tile resident in LDS), -1 = by batch size
- *          (the default; environment SRCNN_L3S sets the initial value).
- * Workspace sizes depend on it: query them after setting it. */
-SRCNN_API int srcnn_set_kernel_option(const char* name, int value);
 
 /* One training step on one device: srcnn_train_fwd_bwd over the batch, then
  * srcnn_update_all(update_batch) -- src/Main_cl.cpp:161-175 (execute_batch

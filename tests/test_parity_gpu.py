@@ -772,48 +772,3 @@ def test_graph_replay_matches_direct_steps(S, batch):
         S.comm_destroy(comms[0])
     with pytest.raises(ValueError):
         S.Graph(lambda: None, None)  # the NULL stream cannot be captured
-
-
-@pytest.mark.parametrize("l3s", [0, 1], ids=["l3_delta", "l3s"])
-@pytest.mark.parametrize("name,batch,size,w", [("default", 16, 33, 33), ("default", 513, 33, 33),
-                                               ("example", 7, 33, 33), ("default_f3", 7, 33, 33),
-                                               ("default", 9, 35, 31), ("default", 1, 33, 33)])
-def test_fused_layer3_kernels_vs_oracle(S, l3s, name, batch, size, w):
-    """Both layer-3 kernels of the fused step (srcnn_set_kernel_option "l3s":
-    l3_delta with the A2 tile in LDS, l3s two-pass streaming), each forced,
-    against the oracle: gradients (fp32 oracle normwise, exact elementwise),
-    squared error, and the A3 each writes to the workspace."""
-    cfg = NETS[name]
-    net = S.Net(*cfg)
-    rng = np.random.default_rng(31 + batch)
-    X, T = make_batch(rng, batch, w, size)
-    params = make_params(rng, cfg, sd=0.05)
-    P = params.size
-    g0 = (1e-3 * rng.standard_normal(P)).astype(np.float32)
-    rg, acts = orc.train_fwd_bwd(cfg, X, T, w, size, batch, params, g0, want_acts=True)
-    xg, _ = orc.f64.train_fwd_bwd(cfg, X, T, w, size, batch, params, g0)
-    S.set_kernel_option("l3s", l3s)
-    try:
-        nbytes = S.train_workspace_bytes(net, w, size, batch)
-        ws = torch.empty(nbytes // 4 + 64, dtype=torch.float32, device="cuda")
-        g, err = D(g0), zeros(1)
-        S.train_fwd_bwd(net, D(X), D(T), w, size, batch, D(params), g, err, ws, nbytes)
-        assert S.last_path() == "fused"
-        n1, n2, f1, f2, f3 = cfg
-        w1, h1 = w - f1 + 1, size - f1 + 1
-        w3, h3 = w1 - f3 + 1, h1 - f3 + 1
-        A1 = zeros(batch * w1 * h1 * n1)
-        A2 = zeros(batch * w1 * h1 * n2)
-        A3 = zeros(batch * w3 * h3)
-        S.train_activations(net, w, size, batch, ws, nbytes, A1, A2, A3)
-        got = H(g)
-    finally:
-        S.set_kernel_option("l3s", -1)
-    off = S.net_offsets(net) + [P]
-    for i, nm in enumerate(["W1", "B1", "W2", "B2", "W3", "B3"]):
-        sl = slice(off[i], off[i + 1])
-        assert_close(got[sl], rg[sl], RTOL, "grad %s (l3s=%d)" % (nm, l3s), xg[sl], FLIP_FLOOR)
-    s1, s2 = batch * w1 * h1 * n1, batch * w1 * h1 * n2
-    assert_close(H(A3), acts[s1 + s2:s1 + s2 + batch * w3 * h3], RTOL, "A3 (l3s=%d)" % l3s)
-    ref_err = orc.sq_err(T, acts[s1 + s2:s1 + s2 + batch * w3 * h3], w, size, w3, h3, batch)
-    assert float(H(err)[0]) == pytest.approx(ref_err, rel=1e-4)

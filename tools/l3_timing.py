@@ -32,8 +32,7 @@ assert S.lib().srcnn_debug_l3_timing(buf) == 0
 t = np.array(buf, dtype=np.float64).reshape(1024, 4)
 t = t[t.sum(axis=1) > 0]
 spb = B / len(t)  # samples per block
-names = (["pass 1", "pass-1 barrier", "window + barrier", "pass 2"] if os.environ.get("SRCNN_L3S_TIMING")
-         else ["Q mfma", "L3 gather+delta3", "delta2+gW3 (wave 0)", "top wait (DMA+barrier)"])
+names = ["Q mfma", "L3 gather+delta3", "delta2+gW3 (wave 0)", "top wait (DMA+barrier)"]
 tot = t.sum(axis=1).mean()
 for i, n in enumerate(names):
     print("%-18s %10.0f cycles/block  %5.1f%%  (%.0f per sample)" % (n, t[:, i].mean(), 100 * t[:, i].mean() / tot, t[:, i].mean() / spb))
