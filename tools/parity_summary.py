@@ -8,14 +8,21 @@ written when SRCNN_PARITY_LOG is set during `pytest -m gpu`):
 Fields: check count, checks against the exact (double-precision) result,
 the largest normwise error, the largest elementwise relative error on
 significant elements, how many checks stay within 1e-4 elementwise, and the
-ten checks with the largest elementwise error.
+ten checks with the largest elementwise error.  The masked-parity tests
+(tests/test_parity_masks_gpu.py) add two kinds of record: ReLU-decision flip
+counts per layer (`flips_A*`, `ambiguous_A*`) and checks whose elements past
+the relative tolerance are judged against the fp32 rounding bound
+(`n_over_rtol`, `rounding_ratio_max`); both are summarised separately.
 """
 import json
 import sys
 
 
 def main(path):
-    recs = [json.loads(l) for l in open(path) if l.strip()]
+    allrecs = [json.loads(l) for l in open(path) if l.strip()]
+    flips = [r for r in allrecs if "flips_A1" in r]
+    recs = [r for r in allrecs if "normwise" in r]
+    bounded = [r for r in recs if "rounding_ratio_max" in r]
     exact = [r for r in recs if r.get("elementwise") is not None]
     out = {
         "checks": len(recs),
@@ -24,6 +31,12 @@ def main(path):
         "max_elementwise_no_floor": max((r["elementwise"] for r in exact if not r.get("abs_floor")), default=None),
         "elementwise_within_1e-4": sum(1 for r in exact if r["elementwise"] <= 1e-4),
         "elementwise_beyond_own_bound": sum(1 for r in exact if r.get("n_over")),
+        "rounding_clause_checks": len(bounded),
+        "rounding_clause_elements_past_rtol": sum(r["n_over_rtol"] for r in bounded),
+        "rounding_ratio_max": max((r["rounding_ratio_max"] for r in bounded), default=None),
+        "flip_records": len(flips),
+        "flips_total": {k: sum(r[k] for r in flips) for k in ("flips_A1", "flips_A2", "flips_A3")},
+        "ambiguous_total": {k: sum(r[k] for r in flips) for k in ("ambiguous_A1", "ambiguous_A2", "ambiguous_A3")},
         "worst": sorted(({k: r[k] for k in ("what", "n", "normwise", "elementwise", "elementwise_fp32_oracle",
                                             "abs_floor") if k in r} for r in exact),
                         key=lambda r: -r["elementwise"])[:10],
