@@ -156,6 +156,22 @@ bool ConfigBasedDataPipeline::bind_flat(LayerAllocationPool& l1, LayerAllocation
     _context->write_buffer(_flat_params, host.data(), true);
     _context->zeros_float(_flat_grads, false);
     _context->zeros_float(_flat_moms, false);
+    bool resume = false;
+    for (int i = 0; i < 3; ++i) resume = resume || !_momentum_in[i][0].empty() || !_momentum_in[i][1].empty();
+    if (resume) {  // momentum saved by write_params_to_file (set_save_momentum)
+      std::vector<float> mom(P, 0.0f);
+      for (int i = 0; i < 3; ++i) {
+        const size_t n[2] = {layers[i]->weight_size(), layers[i]->bias_size()};
+        for (int k = 0; k < 2; ++k) {
+          const auto& v = _momentum_in[i][k];
+          if (v.empty()) continue;
+          srcnn::require(v.size() == n[k], "parameters file: layer " + std::to_string(i + 1) + " momentum has " +
+                                               std::to_string(v.size()) + " values, expected " + std::to_string(n[k]));
+          std::copy(v.begin(), v.end(), mom.begin() + off[2 * i + k]);
+        }
+      }
+      _context->write_buffer(_flat_moms, mom.data(), true);
+    }
     for (int i = 0; i < 3; ++i) {
       size_t wb = layers[i]->weight_size() * sizeof(float), bb = layers[i]->bias_size() * sizeof(float);
       size_t wo = off[2 * i] * sizeof(float), bo = off[2 * i + 1] * sizeof(float);
@@ -375,6 +391,8 @@ size_t ConfigBasedDataPipeline::load_parameters_file(const char* file) {
       for (auto& sub : kv.second.object) {
         try_read_vector(sub.first, sub.second, layers[i]->weights, "weights");
         try_read_vector(sub.first, sub.second, layers[i]->bias, "bias");
+        try_read_vector(sub.first, sub.second, _momentum_in[i][0], "momentum_weights");
+        try_read_vector(sub.first, sub.second, _momentum_in[i][1], "momentum_bias");
       }
     }
     if (!known) std::cout << "[Warning] Unknown key '" << kv.first << "' in parameters file" << std::endl;
@@ -397,6 +415,17 @@ void ConfigBasedDataPipeline::write_params_to_file(const char* path, LayerAlloca
     if (pools[i]->bias != gpu_nullptr)
       _context->read_buffer(pools[i]->bias, 0, d.bias_size() * sizeof(float), d.bias.data(), true);
   }
+  std::vector<float> mom[3][2];
+  if (_save_momentum)
+    for (int i = 0; i < 3; ++i) {
+      const MemoryHandle h[2] = {pools[i]->previous_batch_delta_w, pools[i]->previous_batch_delta_b};
+      const size_t n[2] = {layers[i]->weight_size(), layers[i]->bias_size()};
+      for (int k = 0; k < 2; ++k) {
+        if (h[k] == gpu_nullptr) continue;
+        mom[i][k].resize(n[k]);
+        _context->read_buffer(h[k], 0, n[k] * sizeof(float), mom[i][k].data(), true);
+      }
+    }
   std::ofstream out(path);
   if (!out.is_open()) throw srcnn::IOException(std::string("Could not write parameters file: ") + path);
   auto dump = [&out](const std::vector<float>& v) {
@@ -408,7 +437,18 @@ void ConfigBasedDataPipeline::write_params_to_file(const char* path, LayerAlloca
     dump(layers[i]->weights);
     out << "],\n    \"bias\": [";
     dump(layers[i]->bias);
-    out << "]\n  }" << (i < 2 ? ",\n" : "\n");
+    out << "]";
+    if (!mom[i][0].empty()) {
+      out << ",\n    \"momentum_weights\": [";
+      dump(mom[i][0]);
+      out << "]";
+    }
+    if (!mom[i][1].empty()) {
+      out << ",\n    \"momentum_bias\": [";
+      dump(mom[i][1]);
+      out << "]";
+    }
+    out << "\n  }" << (i < 2 ? ",\n" : "\n");
   }
   out << "}";
 }

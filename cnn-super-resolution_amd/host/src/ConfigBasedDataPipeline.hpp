@@ -99,6 +99,12 @@ class ConfigBasedDataPipeline : public DataPipeline {
   /** seed the random initialisation (the reference seeds with the clock) */
   void set_random_seed(uint64_t seed) { _seed = seed; _seeded = true; }
   size_t epochs() const { return _epochs; }
+  /** opt-in (the reference restarts momentum at zero on resume,
+   * ConfigBasedDataPipeline.cpp:419-465): write_params_to_file() also stores
+   * each layer's momentum ("momentum_weights" / "momentum_bias", keys the
+   * reference's loader skips), and a parameters file that holds them resumes
+   * the pipeline-owned momentum buffers from them */
+  void set_save_momentum(bool on) { _save_momentum = on; }
   /** L3 output of the last forward / execute_batch chunk */
   MemoryHandle result_buffer() const { return _out_3_gpu_buf; }
   /** the flat [gW1|gB1|gW2|gB2|gW3|gB3] buffer (gpu_nullptr before training
@@ -142,6 +148,8 @@ class ConfigBasedDataPipeline : public DataPipeline {
   size_t _mini_batch_size = 0;
   uint64_t _seed = 0;
   bool _seeded = false;
+  bool _save_momentum = false;
+  std::vector<float> _momentum_in[3][2];  // momentum read from the parameters file [layer][W, B]
 
   size_t _buf_w = 0, _buf_h = 0, _buf_n = 0;
   MemoryHandle _ground_truth_gpu_buf = gpu_nullptr;

@@ -3,7 +3,7 @@
 //
 //   cnn [-h] [train] [dry] [profile] -c CONFIG -i IN [-o OUT] [-e EPOCHS]
 //       [--seed N] [--device D] [--devices N] [--validation-percent P]
-//       [--mini-batches M]
+//       [--mini-batches M] [--save-momentum]
 //
 // forward:  IN is an image (JPEG / PNG / PNM), OUT the upscaled result image
 // train:    IN is a directory of <name>_large.<ext> / <name>_small.<ext> pairs
@@ -60,6 +60,7 @@ struct Args {
   bool devices_set = false;  // --devices given: the data-parallel driver (also for N = 1)
   bool host_exchange = false;  // --exchange host: the host-sum test seam instead of RCCL
   bool same_device = false;    // --same-device: every rank on --device (needs --exchange host)
+  bool save_momentum = false;  // --save-momentum: momentum into the parameters file (resumable)
   size_t validation_percent = 20;  // src/Main_cl.cpp:87
   size_t mini_batches = 2;         // src/Main_cl.cpp:88
 };
@@ -68,7 +69,7 @@ void usage() {
   std::cout
       << "usage: cnn [-h] [train] [dry] [profile] -c CONFIG -i IN [-o OUT] [-e EPOCHS]\n"
          "           [--seed N] [--device D] [--devices N] [--validation-percent P]\n"
-         "           [--mini-batches M]\n\n"
+         "           [--mini-batches M] [--save-momentum]\n\n"
          "  -h, --help            print this help\n"
          "  --version             library ABI, HIP runtime and RCCL the binary runs on\n"
          "  train                 train mode\n"
@@ -85,7 +86,9 @@ void usage() {
          "                        host-side sum, a test seam)\n"
          "  --same-device         every data-parallel rank on --device (with --exchange host)\n"
          "  --validation-percent  share of samples used for validation (default 20)\n"
-         "  --mini-batches M      mini-batches per epoch (default 2)\n";
+         "  --mini-batches M      mini-batches per epoch (default 2)\n"
+         "  --save-momentum       also store the momentum in the parameters file; a file\n"
+         "                        that holds it resumes training with it (extension)\n";
 }
 
 bool parse(int argc, char** argv, Args& a) {
@@ -113,6 +116,7 @@ bool parse(int argc, char** argv, Args& a) {
       a.host_exchange = v == "host";
     }
     else if (s == "--same-device") a.same_device = true;
+    else if (s == "--save-momentum") a.save_momentum = true;
     else if (s == "--validation-percent") a.validation_percent = std::stoul(value("--validation-percent"));
     else if (s == "--mini-batches") a.mini_batches = std::stoul(value("--mini-batches"));
     else throw std::runtime_error("unknown argument '" + s + "'");
@@ -267,6 +271,7 @@ int train(ConfigBasedDataPipeline& p, const Args& a, uint64_t shuffle_seed, Grad
                   << " per px)" << std::endl;
     }
   }
+  p.set_save_momentum(a.save_momentum);
   if (lead && !a.dry && !a.out.empty())
     p.write_params_to_file(a.out.c_str(), pools.layer_1, pools.layer_2, pools.layer_3);
   ctx.block();
