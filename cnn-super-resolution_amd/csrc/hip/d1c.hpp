@@ -242,18 +242,58 @@ __global__ __launch_bounds__(256 * kD1cTeams, SRCNN_D1C_OCC) void d1c_grad12_ker
         av[pm][1] = *reinterpret_cast<const f32x4*>(d2b + 512 * pm + r1b1);
         d1[pm] = mfma::zero4();
       }
+      // gW1's pixel -> X-tile offsets of the chunk (k-step k = (pm, i) of
+      // lane group lg is pixel 16 pm + 4 lg + i)
+      const int4 xb4[2] = {*reinterpret_cast<const int4*>(xo + c * 32 + 4 * lg),
+                           *reinterpret_cast<const int4*>(xo + c * 32 + 16 + 4 * lg)};
+      // gW2 operands (k-step s: pixel 4 s + pl) in a ring of three register
+      // sets, read two k-steps ahead of their MFMAs
+      float ga[3], gd[3][2];
+      auto gw2_read = [&](int s_) {
+        ga[s_ % 3] = a1b[64 * s_ + r3b[s_ & 1]];
+#pragma unroll
+        for (int u = 0; u < 2; u++) gd[s_ % 3][u] = d2b[128 * s_ + r2b[u][s_ & 1]];
+      };
+      gw2_read(0);
+      gw2_read(1);
       __builtin_amdgcn_sched_barrier(0);  // keep the reads above issued first
-#pragma unroll
-      for (int s = 0; s < 8; s++)
-#pragma unroll
-        for (int pm = 0; pm < 2; pm++) d1[pm] = mfma::mma16(av[pm][s >> 2][s & 3], w2r[s], d1[pm]);
-
-      // gW2 += A1^T delta2 (k-step s: pixel 4 s + pl)
+      // The MFMA order is pinned (sched_barrier per group): a dependent
+      // v_mfma_f32_16x16x4_f32 issues 40 cycles after its predecessor but an
+      // independent one after 32 (MI355X_MICROARCH.md constants), and left
+      // alone the scheduler chains same-accumulator MFMAs back to back.
+      // delta1: the two pixel tiles alternate
 #pragma unroll
       for (int s = 0; s < 8; s++) {
-        const float a = a1b[64 * s + r3b[s & 1]];
 #pragma unroll
-        for (int u = 0; u < 2; u++) g2[u] = mfma::mma16(a, d2b[128 * s + r2b[u][s & 1]], g2[u]);
+        for (int pm = 0; pm < 2; pm++) d1[pm] = mfma::mma16(av[pm][s >> 2][s & 3], w2r[s], d1[pm]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+
+      // gW1's X gathers: the six values of k-step k (tiles 0-4 and the VALU
+      // tap) in a ring of three register sets, two k-steps ahead; the first
+      // two are issued under gW2's MFMAs
+      float xv[3][6];
+      auto gather = [&](int k) {
+        const int4 v = xb4[k >> 2];
+        const int i = k & 3;
+        const float* xl = xs + (i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w);
+        float* dst = xv[k % 3];
+#pragma unroll
+        for (int m = 0; m < 4; m++) dst[m] = xl[tb + kTileOff[m]];
+        dst[4] = xl[t4];
+        dst[5] = xl[7 * S + 8];
+      };
+
+      // gW2 += A1^T delta2; the two n2 tiles alternate
+#pragma unroll
+      for (int s = 0; s < 8; s++) {
+        if (s + 2 < 8) gw2_read(s + 2);
+        if (s == 4) gather(0);
+        if (s == 6) gather(1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < 2; u++) g2[u] = mfma::mma16(ga[s % 3], gd[s % 3][u], g2[u]);
+        __builtin_amdgcn_sched_barrier(0);
       }
       // gB2 += delta2: wave w sums k-steps 2w, 2w + 1 (balanced; the waves
       // meet at every chunk barrier), the waves' partials are added at the end
@@ -267,27 +307,25 @@ __global__ __launch_bounds__(256 * kD1cTeams, SRCNN_D1C_OCC) void d1c_grad12_ker
 #pragma unroll
         for (int i = 0; i < 4; i++) d1[pm][i] = mk[pm][i] > 0.0f ? d1[pm][i] : 0.0f;
 
-      // gW1 += Xwin^T delta1: k-step (pm, i), lane group lg <-> pixel 16 pm + 4 lg + i
-      // (pixels past the sample map onto its last one: their delta1 is 0)
+      // gW1 += Xwin^T delta1: k-step k = (pm, i), lane group lg <-> pixel
+      // 16 pm + 4 lg + i (pixels past the sample map onto its last one: their
+      // delta1 is 0)
 #pragma unroll
-      for (int pm = 0; pm < 2; pm++) {
-        const int4 xb4 = *reinterpret_cast<const int4*>(xo + c * 32 + 16 * pm + 4 * lg);
+      for (int k = 0; k < 8; k++) {
+        if (k + 2 < 8) gather(k + 2);
+        __builtin_amdgcn_sched_barrier(0);
+        const float bv = d1[k >> 2][k & 3];
+        const float* x = xv[k % 3];
+        if (kD1cDiag & 4) {
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
-          const int xb = i == 0 ? xb4.x : i == 1 ? xb4.y : i == 2 ? xb4.z : xb4.w;
-          const float bv = d1[pm][i];
-          const float* xl = xs + xb;
-          if (kD1cDiag & 4) {
+          for (int m = 0; m < 5; m++) g1[m] = mfma::mma16(bv + m, bv, g1[m]);
+        } else {
 #pragma unroll
-            for (int m = 0; m < 5; m++) g1[m] = mfma::mma16(bv + m, bv, g1[m]);
-          } else {
-#pragma unroll
-            for (int m = 0; m < 4; m++) g1[m] = mfma::mma16(xl[tb + kTileOff[m]], bv, g1[m]);
-            g1[4] = mfma::mma16(xl[t4], bv, g1[4]);
-          }
-          gv = fmaf(xl[7 * S + 8], bv, gv);
-          gvb += bv;
+          for (int m = 0; m < 5; m++) g1[m] = mfma::mma16(x[m], bv, g1[m]);
         }
+        gv = fmaf(x[5], bv, gv);
+        gvb += bv;
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
   }
