@@ -391,6 +391,10 @@ def test_preload_every_net(S):
                                              # ragged against the grids: l3 (256 blocks, walks the
                                              # batch from its end), l12 / d1 (512 blocks)
                                              ("default", 257, 33), ("default", 513, 33),
+                                             # the strong-scaling shard (512 tiles per rank) and its
+                                             # neighbours; below 1024 samples d1c splits each
+                                             # sample's chunks over 2 (511, 512) or 4 (100) blocks
+                                             ("default", 511, 33), ("default", 512, 33), ("default", 100, 33),
                                              # d1c (1024 blocks, 4 samples each at batch 4096)
                                              ("default", 1025, 33), ("default", 5, 39),
                                              # tiles past l3_delta's LDS image (33x33): l12 +
