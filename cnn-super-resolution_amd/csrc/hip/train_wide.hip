@@ -458,16 +458,30 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restri
           const int pix = p0 + crow(r, 0);
           acc[m][r] = (pix < g.npx && mk[r] > 0.0f) ? acc[m][r] : 0.0f;
         }
-#pragma unroll
-        for (int r = 0; r < 16; r++) {
+        // X windows of k-step r (pixel crow(r, h) of the tile) read two k-steps
+        // ahead into a ring of three named register sets, pinned by
+        // sched_barriers: left alone, the scheduler reads each window right
+        // before its MFMA and this one wave per SIMD waits out the LDS latency
+        float xq[3][TT];
+        auto xrd = [&](int r) {
           const int pix = min(p0 + crow(r, 0), g.npx - 1), py = pix / g.out_w;
           const int xb = py * kXS + pix - py * g.out_w;
 #pragma unroll
+          for (int tt = 0; tt < TT; tt++) xq[r % 3][tt] = xs[xb + toffx[tt]];
+        };
+        xrd(0);
+        xrd(1);
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+          if (r + 2 < 16) xrd(r + 2);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
           for (int tt = 0; tt < TT; tt++) {
-            const float av = xs[xb + toffx[tt]];
+            const float av = xq[r % 3][tt];
             if (!(kWDiag & 1)) gacc[tt] = mma(valid[tt] ? av : fill[tt], acc[m][r], gacc[tt]);
             else gacc[tt][0] += acc[m][r] + av;
           }
+          __builtin_amdgcn_sched_barrier(0);
         }
         if (m + 1 < MT) {
 #pragma unroll
@@ -799,16 +813,30 @@ __global__ __launch_bounds__(512, 1) void wgrad2_kernel(const float* __restrict_
     if (!(kWg2Diag & 4) || u == 0) __syncthreads();  // unit u landed; everyone is done with the other buffer
     const float* cur = smem + (bsel ? kGBuf : 0);
     if (u + 1 < nunits && !(kWg2Diag & 2)) stage(u + 1, smem + (bsel ? 0 : kGBuf));
+    // k-step kq's operands (delta2 value + the F*F A1 taps) are read one
+    // k-step ahead into two named register sets, pinned by sched_barriers:
+    // left alone, the scheduler reads two taps at a time right before their
+    // MFMA pair and waits out the LDS latency every other MFMA
+    float av[2][FF], bv[2];
+    auto rd = [&](int kq) {
+      bv[kq & 1] = cur[dlane + kq * 4 * kGDS];
+#pragma unroll
+      for (int t = 0; t < FF; t++) av[kq & 1][t] = cur[abase[kq] + ((t / F) * aw + t % F) * kGAS];
+    };
+    rd(0);
 #pragma unroll
     for (int kq = 0; kq < 16; kq++) {
-      const float b = cur[dlane + kq * 4 * kGDS];
+      if (kq + 1 < 16) rd(kq + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      const float b = bv[kq & 1];
       if (gbw) gb += b;
 #pragma unroll
       for (int t = 0; t < FF; t++) {
-        const float a = cur[abase[kq] + ((t / F) * aw + t % F) * kGAS];
+        const float a = av[kq & 1][t];
         if (kWg2Diag & 1) acc[t][0] += a * b;
         else acc[t] = mma16(a, b, acc[t]);
       }
+      __builtin_amdgcn_sched_barrier(0);
     }
     bsel ^= 1;
   }

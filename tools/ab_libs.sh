@@ -18,6 +18,6 @@ for rep in 1 2; do
   for lib in "$@"; do
     i=$((i+1))
     SRCNN_HIP_LIB=$PWD/$lib timeout -k 10 180 python bench.py --no-cpu-baseline > "$OUT/bench_${i}_$rep.json" 2>"$OUT/bench_${i}_$rep.err" || exit $?
-    python3 -c "import json; d=json.load(open('$OUT/bench_${i}_$rep.json')); print('variant $i rep $rep', round(d['value']), d['ms_per_step'], {k:round(v['ms_per_step'],4) for k,v in d['kernels'].items()})"
+    python3 -c "import json; d=json.load(open('$OUT/bench_${i}_$rep.json')); print('variant $i rep $rep', round(d['value']), d['ms_per_step'], {k:round(v['ms_per_step'],4) for k,v in d['kernels'].items()}, 'wide', d.get('wide',{}).get('ms_per_step'), {k:round(v['ms_per_step'],4) for k,v in d.get('wide',{}).get('kernels',{}).items()})"
   done
 done
