@@ -201,8 +201,8 @@ __global__ void prepack_w2_kernel(const float* __restrict__ W2, float* __restric
 // live in registers across the K loop (CIN/16 chunks x F*F taps x 2).
 // Each chunk's image (img_w x img_h pixels x 16 channels, 80-B rows) is
 // staged by LDS-DMA into the other buffer while the current one is consumed;
-// the DMA instructions are spread over the first k-steps, issued after the
-// k-step's B load so that B waits never cover a fresh DMA.
+// the DMA instructions go out as one burst in the chunk's first tap, after
+// that tap's B loads, so only the B waits of tap 4 cover them.
 // ---------------------------------------------------------------------------
 constexpr int kImgMax = 960;                  // pixels of one chunk image (<= 31 x 31)
 constexpr int kImgSlack = 256;                // floats: one DMA instruction past the image
@@ -391,12 +391,15 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restri
 #pragma unroll
           for (int q = 0; q < 2; q++)
             bq[(dx + F - 1) % F][q] = wp[(size_t)min(ksb + q, KS - 1) * 64];
-          // this tap's share of the next chunk's DMA (issued after the B loads)
-#pragma unroll
-          for (int q = 0; q < 2; q++) {
-            const int k = wave + 4 * (2 * t + q);
-            if (stage && k < kdma && !(kWDiag & 4)) dma(wd, nc, nxt, k);
-          }
+          // the next chunk's whole DMA in the first tap, after its B loads.
+          // The DMA is inline asm, invisible to the compiler's vmcnt counting,
+          // so each vmcnt(8) it emits for a B-ring load 4 taps back also
+          // waits for every DMA issued after that load: spread over the first
+          // taps (2 per tap), the DMAs were waited on 3 taps after issue; as
+          // one burst at tap 0 only the B loads of tap 4 wait for them
+          // (same-box A/B: delta1 + gW1 -1.0%, L2 forward -1.0%)
+          if (t == 0 && stage && !(kWDiag & 4))
+            for (int k = wave; k < kdma; k += 4) dma(wd, nc, nxt, k);
           // k-step (t, 0) while (t, 1) loads; k-step (t, 1) while (t + 1, 0)
           // loads.  sched_barriers pin the order: left alone, the scheduler
           // sinks the prefetch reads below the MFMAs and exposes LDS latency.
