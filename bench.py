@@ -530,8 +530,12 @@ def main():
     ap.add_argument("--comm", choices=["srcnn", "torch"], default="srcnn")
     # the timed steps replay one HIP graph of the step (srcnn_graph_*): the
     # same kernels and collective without a host launch per kernel.  Default:
-    # on for N > 1 (no host launch jitter between the ranks' collectives), off
-    # for N = 1, where it measured the same (0.8975 vs 0.894 ms, same box)
+    # on for N > 1 with --global-batch (strong scaling: small per-rank steps,
+    # where host launch jitter between the ranks' collectives shows), off
+    # otherwise: at N = 1 it measured the same (0.8975 vs 0.894 ms, same box),
+    # and at 4096 tiles per rank the launches hide under the kernels, so the
+    # weak-scaling line keeps the direct calls (a captured multi-rank RCCL
+    # collective has only been replayed on a one-rank communicator here)
     ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default=None,
                     help="process-group backend (default: gloo with --comm srcnn, nccl with torch)")
@@ -630,7 +634,8 @@ def main():
             _mark("first warmup step enqueued")
     torch.cuda.synchronize()
     _mark("warmup done")
-    use_graph = (args.graph == "on" or (args.graph == "auto" and world > 1)) and (world == 1 or comm is not None)
+    use_graph = (args.graph == "on" or (args.graph == "auto" and world > 1 and strong)) and \
+        (world == 1 or comm is not None)
     graph = None
     if use_graph:
         try:
