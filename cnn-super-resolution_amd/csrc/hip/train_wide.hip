@@ -612,8 +612,17 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restri
 // gW3 / gB3 / squared error accumulate in registers across the block's
 // samples and leave as one slab per block.
 // ---------------------------------------------------------------------------
+// Operands run ahead of their use (round 3, -18% wl3): each wave's next Q
+// tile (across samples: the next sample's first tile) is in flight under the
+// current tile's MFMAs, and gW3's A2 pixel pairs come in batches of kWl3B, the
+// next batch in flight under the current one.  Two blocks per CU, every
+// accumulator in VGPRs (launch bound).
+#ifndef SRCNN_WL3_B
+#define SRCNN_WL3_B 4  // gW3 pixel pairs per prefetch batch
+#endif
+constexpr int kWl3B = SRCNN_WL3_B;
 template <int N2, int F3>
-__global__ __launch_bounds__(256) void wl3_kernel(const float* __restrict__ A2,
+__global__ __launch_bounds__(256, 2) void wl3_kernel(const float* __restrict__ A2,
                                                   const float* __restrict__ T,
                                                   const float* __restrict__ W3,
                                                   const float* __restrict__ B3,
@@ -657,16 +666,26 @@ __global__ __launch_bounds__(256) void wl3_kernel(const float* __restrict__ A2,
   f32x16 gacc0 = zero16(), gacc1 = zero16();
   float sq = 0.0f, gb3 = 0.0f;
   const float b3 = B3[0];
+  // step 1 operands of tile mt: lane (j, h) reads pixel 32 mt + j, channels
+  // 8 kk + 4 h + jj.  The next tile's (across samples: the next sample's first
+  // tile's) loads are in flight under the current tile's MFMAs.
+  float4 vn[8];
+  auto ldq = [&](const float* a2s_, int mt_) {
+    const int p = min(32 * mt_ + j, npx2 - 1);
+    const float4* src = reinterpret_cast<const float4*>(a2s_ + (size_t)p * N2) + h;
+#pragma unroll
+    for (int kk = 0; kk < 8; kk++) vn[kk] = src[2 * kk];
+  };
+  if ((int)blockIdx.x < g.batch && wave < mt2) ldq(A2 + (size_t)blockIdx.x * npx2 * N2, wave);
   for (int s = blockIdx.x; s < g.batch; s += gridDim.x) {
     const float* a2s = A2 + (size_t)s * npx2 * N2;
     __syncthreads();  // previous sample's Gd / Qs readers are done
     // 1. Q
     for (int mt = wave; mt < mt2; mt += 4) {
-      const int p = min(32 * mt + j, npx2 - 1);
-      const float4* src = reinterpret_cast<const float4*>(a2s + (size_t)p * N2) + h;
       float4 v[8];
 #pragma unroll
-      for (int kk = 0; kk < 8; kk++) v[kk] = src[2 * kk];
+      for (int kk = 0; kk < 8; kk++) v[kk] = vn[kk];
+      if (mt + 4 < mt2) ldq(a2s, mt + 4);
       f32x16 acc = zero16();
 #pragma unroll
       for (int kk = 0; kk < 8; kk++)
@@ -721,16 +740,41 @@ __global__ __launch_bounds__(256) void wl3_kernel(const float* __restrict__ A2,
         }
       }
     }
-    // 4. gW3 (K = pixel pairs split over the waves; B columns: channel 2j + tile)
-    for (int kp = wave; 2 * kp < npx2; kp += 4) {
-      const int pk = 2 * kp + h;
-      const bool pok = pk < npx2;
-      const int p = pok ? pk : npx2 - 1, py = p / g.w2, px = p - py * g.w2;
-      const float av = Gd[(py + F3 - 1) * GW + px + F3 - 1 + goffA];
-      const float a = (tapA && pok) ? av : 0.0f;
-      const float2 bv = *reinterpret_cast<const float2*>(a2s + (size_t)p * N2 + 2 * j);
-      gacc0 = mma(a, bv.x, gacc0);
-      gacc1 = mma(a, bv.y, gacc1);
+    // the next sample's first Q tile, in flight under delta2 / gW3
+    if (s + (int)gridDim.x < g.batch && wave < mt2) ldq(a2s + (size_t)gridDim.x * npx2 * N2, wave);
+    // 4. gW3 (K = pixel pairs kp = wave + 4 i split over the waves; B columns:
+    // channel 2j + tile), in batches of kWl3B pairs: the next batch's A2 loads
+    // and delta3-window reads are issued before the current batch's MFMAs
+    // (two named register sets); pairs past the wave's count are not issued
+    const int niter = (npx2 + 1) / 2 > wave ? ((npx2 + 1) / 2 - wave + 3) / 4 : 0;
+    float2 bb[2][kWl3B];
+    float ab[2][kWl3B];
+    auto ldb = [&](int i0, float2 (&b_)[kWl3B], float (&a_)[kWl3B]) {
+#pragma unroll
+      for (int u = 0; u < kWl3B; u++) {
+        const int pk = 2 * (wave + 4 * (i0 + u)) + h;
+        const bool pok = pk < npx2;
+        const int p = pok ? pk : npx2 - 1, py = p / g.w2, px = p - py * g.w2;
+        const float av = Gd[(py + F3 - 1) * GW + px + F3 - 1 + goffA];
+        a_[u] = (tapA && pok) ? av : 0.0f;
+        b_[u] = *reinterpret_cast<const float2*>(a2s + (size_t)p * N2 + 2 * j);
+      }
+    };
+    auto mmb = [&](int i0, const float2 (&b_)[kWl3B], const float (&a_)[kWl3B]) {
+#pragma unroll
+      for (int u = 0; u < kWl3B; u++)
+        if (i0 + u < niter) {
+          gacc0 = mma(a_[u], b_[u].x, gacc0);
+          gacc1 = mma(a_[u], b_[u].y, gacc1);
+        }
+    };
+    if (niter > 0) ldb(0, bb[0], ab[0]);
+    for (int i0 = 0; i0 < niter; i0 += 2 * kWl3B) {
+      if (i0 + kWl3B < niter) ldb(i0 + kWl3B, bb[1], ab[1]);
+      mmb(i0, bb[0], ab[0]);
+      if (i0 + kWl3B >= niter) break;
+      if (i0 + 2 * kWl3B < niter) ldb(i0 + 2 * kWl3B, bb[0], ab[0]);
+      mmb(i0 + kWl3B, bb[1], ab[1]);
     }
   }
   // cross-wave reduction of gW3 (fixed order), gB3, squared error
