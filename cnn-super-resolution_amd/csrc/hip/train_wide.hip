@@ -88,13 +88,16 @@ struct WGeom {
 // GEMM M = pixels (32-row tiles), N = 4 x 32 channels (one tile per wave),
 // K = 81 taps (+1 zero tap).  The k-slot pairing gives half h the taps
 // [KP*h, KP*h + KP), so every A operand is one ds_read_b32 at a per-half base
-// plus an immediate.
+// plus an immediate.  Four blocks per CU (launch bound: 120 VGPRs), so the
+// 1024-block grid is resident at once and every block gets the same number
+// of samples (at three blocks per CU, 256 of the 1024 ran after the rest:
+// 0.509 -> 0.486 ms, profiles/r03_ab_wl1).
 // ---------------------------------------------------------------------------
 constexpr int kXS = 40;                // LDS row stride of an X tile (w, h <= kXS)
 constexpr int kXTile = kXS * (kXS + 1);  // + one zero row read by the padded tap
 
 template <int N1, int F1>
-__global__ __launch_bounds__(256) void wl1_fwd_kernel(const float* __restrict__ X,
+__global__ __launch_bounds__(256, 4) void wl1_fwd_kernel(const float* __restrict__ X,
                                                       const float* __restrict__ W1,
                                                       const float* __restrict__ B1,
                                                       float* __restrict__ A1, WGeom g) {
