@@ -165,7 +165,9 @@ __global__ __launch_bounds__(256, 4) void wl1_fwd_kernel(const float* __restrict
 constexpr int kCC = 16;       // input channels per LDS chunk
 constexpr int kPS = kCC + 4;  // LDS floats per staged pixel (80 B rows)
 
-template <int CIN, int COUT, int F>
+// D16: the delta1 image for d1g16_kernel instead: [n16][chunk][tap][lane][jj],
+// lane (n = lane & 15, g = lane >> 4) holding W2[flip(tap)][16 n16 + n][16 chunk + 4 g + jj]
+template <int CIN, int COUT, int F, bool D16 = false>
 __global__ void prepack_w2_kernel(const float* __restrict__ W2, float* __restrict__ Wf,
                                   float* __restrict__ Wd) {
   constexpr int FF = F * F, TOT = FF * CIN * COUT;
@@ -176,6 +178,15 @@ __global__ void prepack_w2_kernel(const float* __restrict__ W2, float* __restric
   const int jj = i & 3, lane = (i >> 2) & 63, j = lane & 31, hh = lane >> 5;
   const int rest = i >> 8;
   constexpr int KSC = FF * (kCC / 8);
+  if (D16 && delta) {
+    constexpr int NCH = COUT / kCC;  // delta2 channel chunks
+    const int t = rest % FF, chunk = (rest / FF) % NCH, n16 = rest / (FF * NCH);
+    const int dy = t / F, dx = t - (t / F) * F, tf = (F - 1 - dy) * F + (F - 1 - dx);
+    const int c = chunk * kCC + 4 * (lane >> 4) + jj;  // delta2 channel (n2)
+    const int n = 16 * n16 + (lane & 15);               // delta1 channel (n1)
+    Wd[i] = W2[((size_t)tf * CIN + n) * COUT + c];
+    return;
+  }
   if (!delta) {
     constexpr int KS = (CIN / kCC) * KSC;
     const int ks = rest % KS, nt = rest / KS;
@@ -600,6 +611,325 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restri
           const float v = gacc[tt][r] + red[((nt * TT + tt) * 16 + r) * 64 + lane];
           if (tap <= NT1) o1[tap * COUT + ch] = v;
         }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// d1g16: delta1 + gW1 of the wide training step on 16-pixel M tiles (round 3).
+// The same contraction as conv_mfma<DELTA, F1> (delta1 = relu'(A1) * (delta2
+// padded by F-1 (*) W2 flipped / transposed), then gW1 += Xwin^T delta1 and
+// gB1 from a ones row), on v_mfma_f32_16x16x4_f32 instead of 32x32x2: the
+// same FLOPs per cycle and the same operand reads per MAC, but the border
+// taps are skipped per 16-pixel tile instead of per 32-pixel tile.  The 625
+// output pixels sit in 40 tiles in the class-grouped order of conv_mfma
+// (12,768 -> 11,968 issued pixel-taps for 11,025 useful ones).
+//   work item = (sample, 64 output channels); wave = (nt: 32 of them as two
+//   16-wide N tiles, mg: the M tiles 2m + mg, m < 20)
+//   k-step (tap, 16-channel chunk): A = one ds_read_b128 per lane and tile
+//   (lane (i, g): pixel i of the tile, channels 4g .. 4g + 3 of the chunk),
+//   feeding 4 MFMAs per N tile; B = one float4 per lane and N tile from the
+//   D16 image (prepack_w2_kernel), in a 5-tap ring 4 taps ahead
+//   the tiles run in two halves of 10: one half's MFMAs while the other
+//   half's A operands load
+//   epilogue per tile: C register r of lane (n, g) is pixel slot 4g + r of
+//   channel n, i.e. directly gW1's B operand (K = the 4 pixel slots); A = the
+//   X windows of 16-tap tiles (81 taps + the ones row: 6 tiles)
+// ---------------------------------------------------------------------------
+#ifndef SRCNN_WIDE_D16
+#define SRCNN_WIDE_D16 1
+#endif
+constexpr bool kWideD16 = SRCNN_WIDE_D16;
+constexpr int kD16MT = 20;                   // 16-pixel tiles per wave group
+constexpr int kD16Slots = 2 * kD16MT * 16;  // pixel slots of the tile table
+template <int CIN, int COUT, int F, int F1>
+__global__ __launch_bounds__(256, 1) void d1g16_kernel(const float* __restrict__ in,
+                                                      const float* __restrict__ Wimg,
+                                                      const float* __restrict__ ycur,
+                                                      const float* __restrict__ X,
+                                                      float* __restrict__ slab1, CGeom g) {
+  constexpr int NCH = CIN / kCC, FF = F * F, NP = COUT / 64, MT = kD16MT, MH = MT / 2;
+  // gW1: taps 0 .. 16 TT - 1 on the matrix core, the last tap and gB1 by VALU
+  constexpr int NT1 = F1 * F1, TT = (NT1 - 1) / 16, P1 = NT1 * COUT + COUT;
+  static_assert(CIN % kCC == 0 && COUT % 64 == 0 && F == 5 && MT % 2 == 0 && NT1 == 16 * TT + 1, "shape");
+  extern __shared__ float smem[];
+  const int lane = lane_id(), wave = wave_id(), i16 = lane & 15, g4 = lane >> 4;
+  const int nt = wave & 1, mg = wave >> 1;
+  const int buf_floats = g.img_w * g.img_h * kPS + kImgSlack;
+  const int nitems = g.batch * NP;
+  float* const xsm = smem + 2 * buf_floats;  // 2 X tile buffers (item parity)
+  int* const ptab = reinterpret_cast<int*>(xsm + 2 * kXBuf);
+  // gW1 A operand: tap 16 tt + i16; tap NT1 - 1 (offset toffl) and gB1 by VALU
+  int toffx[TT];
+#pragma unroll
+  for (int tt = 0; tt < TT; tt++) {
+    const int tap = 16 * tt + i16;
+    toffx[tt] = (tap / F1) * kXS + tap % F1;
+  }
+  constexpr int toffl = ((NT1 - 1) / F1) * kXS + (NT1 - 1) % F1;
+  f32x4 gacc[TT][2];
+#pragma unroll
+  for (int tt = 0; tt < TT; tt++) gacc[tt][0] = gacc[tt][1] = zero4();
+  float gv[2] = {0.0f, 0.0f}, gvb[2] = {0.0f, 0.0f};
+  auto xdma = [&](int it, int par) {
+    const int s = it / NP;
+    float* dst = xsm + par * kXBuf;
+    for (int k = wave; k * 64 < kXTile; k += 4) {
+      const int f = k * 64 + lane, row = f / kXS, col = f - row * kXS;
+      const bool ok = row < g.xh && col < g.xw;
+      dma4(ok ? X + (size_t)s * g.xw * g.xh + row * g.xw + col : g_zero_src, dst + k * 64);
+    }
+  };
+  // slot -> pixel table in the class-grouped order (conv_mfma), then each
+  // 16-slot tile's mask of the taps any of its pixels can use
+  const int ow = g.out_w, oh = g.out_h;
+  if (threadIdx.x == 0) {
+    constexpr int B = F - 1;
+    int n = 0;
+    if (ow < 2 * B + 1 || oh < 2 * B + 1) {
+      for (; n < ow * oh && n < kD16Slots; n++) ptab[n] = n;  // raster order
+    } else {
+      auto lo = [&](int c, int e) { return c < B ? c : (c == B ? B : e - 2 * B - 1 + c); };
+      auto hi = [&](int c, int e) { return c < B ? c + 1 : (c == B ? e - B : e - 2 * B + c); };
+      for (int yo = 0; yo <= 2 * B; yo++) {
+        const int yc = yo == 0 ? B : (yo <= B ? yo - 1 : yo);
+        for (int xc = 0; xc <= 2 * B; xc++)
+          for (int x = lo(xc, ow); x < hi(xc, ow); x++)
+            for (int y = lo(yc, oh); y < hi(yc, oh); y++) ptab[n++] = y * ow + x;
+      }
+    }
+    for (; n < kD16Slots; n++) ptab[n] = ow * oh - 1;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kD16Slots; i += 256) {
+    const int pix = ptab[i], y = pix / ow, x = pix - y * ow;
+    uint32_t mb = 0;
+#pragma unroll
+    for (int dy = 0; dy < F; dy++)
+#pragma unroll
+      for (int dx = 0; dx < F; dx++) {
+        const bool ok = y + dy >= g.pad && y + dy < g.pad + g.in_h && x + dx >= g.pad && x + dx < g.pad + g.in_w;
+        mb |= ok ? 1u << (dy * F + dx) : 0u;
+      }
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) mb |= __shfl_xor(mb, o, 64);
+    if ((i & 15) == 0) ptab[kD16Slots + i / 16] = (int)mb;
+  }
+  __syncthreads();
+  // tile order: position 2m + mg <- class-order tile perm[2m + mg], dealt by
+  // tap count (most first) to the wave group with fewer taps so far and room
+  // left, so the two groups issue equally many MFMAs (25x25: 375 / 373 tile-taps
+  // instead of 377 / 371 for alternate tiles)
+  int* const perm = ptab + kD16Slots + 2 * MT;
+  if (threadIdx.x == 0) {
+    int cnt[2] = {0, 0}, sum[2] = {0, 0};
+    for (int pc = FF; pc >= 0; pc--)
+      for (int t = 0; t < 2 * MT; t++)
+        if (__popc((uint32_t)ptab[kD16Slots + t]) == pc) {
+          const int k = (cnt[1] >= MT || (cnt[0] < MT && sum[0] <= sum[1])) ? 0 : 1;
+          perm[2 * cnt[k] + k] = t;
+          cnt[k]++;
+          sum[k] += pc;
+        }
+  }
+  __syncthreads();
+  uint32_t tmask[MT];
+  int abase[MT], tbase[MT];  // tbase: first slot of the tile at position 2m + mg
+#pragma unroll
+  for (int m = 0; m < MT; m++) {
+    const int T = __builtin_amdgcn_readfirstlane(perm[2 * m + mg]);
+    tbase[m] = 16 * T;
+    tmask[m] = __builtin_amdgcn_readfirstlane(ptab[kD16Slots + T]);
+    const int o = ptab[16 * T + i16], oy = o / ow;
+    abase[m] = (oy * g.img_w + o - oy * ow) * kPS + 4 * g4;
+  }
+  auto dma = [&](int s, int c, float* buf, int k) {
+    const int slot = k * 64 + lane;
+    const int pix = slot / 5, q = slot - 5 * pix;
+    const int iy = pix / g.img_w, ix = pix - iy * g.img_w;
+    const int y = iy - g.pad, x = ix - g.pad;
+    const bool ok = q < 4 && slot < g.img_w * g.img_h * 5 && y >= 0 && y < g.in_h && x >= 0 && x < g.in_w;
+    const float* src = ok ? in + ((size_t)(s * g.in_h + y) * g.in_w + x) * CIN + c * kCC + 4 * q : g_zero_src;
+    dma16(src, buf + k * 256);
+  };
+  const int kdma = (g.img_w * g.img_h * 5 + 63) / 64;
+  float* const buf0 = smem;
+  float* const buf1 = smem + buf_floats;
+  if ((int)blockIdx.x < nitems)
+    for (int k = wave; k < kdma; k += 4) dma(blockIdx.x / NP, 0, buf0, k);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int bsel = 0, ipar = 0;
+  for (int it = blockIdx.x; it < nitems; it += gridDim.x, ipar ^= 1) {
+    const int s = it / NP, part = it - s * NP;
+    xdma(it, ipar);  // lands before the first chunk barrier
+    // B: N tile q of this wave is n16 = 4 part + 2 nt + q
+    const float4* wp = reinterpret_cast<const float4*>(Wimg) + (size_t)(4 * part + 2 * nt) * NCH * FF * 64 + lane;
+    constexpr int WQ = NCH * FF * 64;  // float4s between the two N tiles
+    f32x4 acc[MT][2];
+#pragma unroll
+    for (int m = 0; m < MT; m++) acc[m][0] = acc[m][1] = zero4();
+    float4 bq[F][2];
+#pragma unroll
+    for (int d = 0; d < F - 1; d++)
+#pragma unroll
+      for (int q = 0; q < 2; q++) bq[d][q] = wp[(size_t)q * WQ + d * 64];
+    for (int c = 0; c < NCH; c++) {
+      const float* cur = bsel ? buf1 : buf0;
+      float* nxt = bsel ? buf0 : buf1;
+      int nit = it, nc = c + 1;
+      if (nc == NCH) {
+        nit = it + gridDim.x;
+        nc = 0;
+      }
+      const bool stage = nit < nitems;
+      float4 a[MH], an[MH];
+#pragma unroll
+      for (int m = 0; m < MH; m++) a[m] = *reinterpret_cast<const float4*>(cur + abase[m]);
+#pragma unroll 1
+      for (int dy = 0; dy < F; dy++) {
+#pragma unroll
+        for (int dx = 0; dx < F; dx++) {
+          const int t = dy * F + dx;
+          const int toff = (dy * g.img_w + dx) * kPS;
+          const int tn = dx + 1 < F ? t + 1 : (dy + 1 < F ? t + 1 : t);
+          const int toffn = ((tn / F) * g.img_w + (tn % F)) * kPS;
+          // B of tap t + 4 (this chunk or the next) into the slot tap t - 1 used
+          const int kb = min(c * FF + t + F - 1, NCH * FF - 1);
+#pragma unroll
+          for (int q = 0; q < 2; q++) bq[(dx + F - 1) % F][q] = wp[(size_t)q * WQ + kb * 64];
+          // the next chunk's whole DMA in the first tap, after its B loads (conv_mfma)
+          if (t == 0 && stage)
+            for (int k = wave; k < kdma; k += 4) dma(nit / NP, nc, nxt, k);
+          // tiles MH.. of tap t load while tiles ..MH of tap t run
+#pragma unroll
+          for (int m = 0; m < MH; m++) an[m] = *reinterpret_cast<const float4*>(cur + abase[MH + m] + toff);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int m = 0; m < MH; m++)
+            if ((tmask[m] >> t) & 1u) {
+#pragma unroll
+              for (int jj = 0; jj < 4; jj++)
+#pragma unroll
+                for (int q = 0; q < 2; q++) acc[m][q] = mma16(a[m][jj], bq[dx][q][jj], acc[m][q]);
+            }
+          __builtin_amdgcn_sched_barrier(0);
+          // tiles ..MH of tap t + 1 load while tiles MH.. of tap t run
+#pragma unroll
+          for (int m = 0; m < MH; m++) a[m] = *reinterpret_cast<const float4*>(cur + abase[m] + toffn);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int m = 0; m < MH; m++)
+            if ((tmask[MH + m] >> t) & 1u) {
+#pragma unroll
+              for (int jj = 0; jj < 4; jj++)
+#pragma unroll
+                for (int q = 0; q < 2; q++) acc[MH + m][q] = mma16(an[m][jj], bq[dx][q][jj], acc[MH + m][q]);
+            }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      bsel ^= 1;
+    }
+    // epilogue: delta1 = relu'(A1) * acc, then gW1 += Xwin^T delta1
+    const float* xs = xsm + ipar * kXBuf;
+    const size_t obase = (size_t)s * g.npx * COUT + part * 64 + nt * 32 + i16;
+    float mk[2][4], mkn[2][4];
+    auto ldmask = [&](int m, float (&d)[2][4]) {
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int pix = ptab[tbase[m] + 4 * g4 + r];
+#pragma unroll
+        for (int q = 0; q < 2; q++) d[q][r] = ycur[obase + (size_t)pix * COUT + 16 * q];
+      }
+    };
+    ldmask(0, mk);
+#pragma unroll
+    for (int m = 0; m < MT; m++) {
+      if (m + 1 < MT) ldmask(m + 1, mkn);
+      const int s0 = tbase[m] + 4 * g4;
+#pragma unroll
+      for (int r = 0; r < 4; r++)
+#pragma unroll
+        for (int q = 0; q < 2; q++) acc[m][q][r] = (s0 + r < g.npx && mk[q][r] > 0.0f) ? acc[m][q][r] : 0.0f;
+      // X windows of k-step r (pixel slot s0 + r), one k-step ahead, two named sets
+      float xq[2][TT + 1];
+      auto xrd = [&](int r) {
+        const int pix = ptab[s0 + r], py = pix / ow;
+        const int xb = py * kXS + pix - py * ow;
+#pragma unroll
+        for (int tt = 0; tt < TT; tt++) xq[r & 1][tt] = xs[xb + toffx[tt]];
+        xq[r & 1][TT] = xs[xb + toffl];
+      };
+      xrd(0);
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        if (r + 1 < 4) xrd(r + 1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int tt = 0; tt < TT; tt++)
+#pragma unroll
+          for (int q = 0; q < 2; q++) gacc[tt][q] = mma16(xq[r & 1][tt], acc[m][q][r], gacc[tt][q]);
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+          gv[q] = fmaf(xq[r & 1][TT], acc[m][q][r], gv[q]);
+          gvb[q] += acc[m][q][r];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (m + 1 < MT) {
+#pragma unroll
+        for (int q = 0; q < 2; q++)
+#pragma unroll
+          for (int r = 0; r < 4; r++) mk[q][r] = mkn[q][r];
+      }
+    }
+  }
+  // the VALU rows summed over the four pixel-slot groups (fixed order)
+#pragma unroll
+  for (int q = 0; q < 2; q++) {
+    gv[q] += __shfl_xor(gv[q], 16, 64);
+    gv[q] += __shfl_xor(gv[q], 32, 64);
+    gvb[q] += __shfl_xor(gvb[q], 16, 64);
+    gvb[q] += __shfl_xor(gvb[q], 32, 64);
+  }
+  // gW1 slab of this block pair: waves mg = 1 park their partials in LDS,
+  // waves mg = 0 add them (fixed order) and store rows tap < NT1 and gB1
+  __syncthreads();
+  float* red = smem;
+  constexpr int RV = 2 * TT * 2 * 4 * 64;  // the VALU rows' parking place
+  if (mg == 1) {
+#pragma unroll
+    for (int tt = 0; tt < TT; tt++)
+#pragma unroll
+      for (int q = 0; q < 2; q++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) red[(((nt * TT + tt) * 2 + q) * 4 + r) * 64 + lane] = gacc[tt][q][r];
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+      red[RV + ((nt * 2 + q) * 2 + 0) * 64 + lane] = gv[q];
+      red[RV + ((nt * 2 + q) * 2 + 1) * 64 + lane] = gvb[q];
+    }
+  }
+  __syncthreads();
+  if (mg == 0) {
+    float* o1 = slab1 + (size_t)(blockIdx.x / NP) * P1;
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+      const int ch = (blockIdx.x % NP) * 64 + 32 * nt + 16 * q + i16;
+#pragma unroll
+      for (int tt = 0; tt < TT; tt++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int tap = 16 * tt + 4 * g4 + r;
+          o1[tap * COUT + ch] = gacc[tt][q][r] + red[(((nt * TT + tt) * 2 + q) * 4 + r) * 64 + lane];
+        }
+      if (g4 == 0) {
+        o1[(NT1 - 1) * COUT + ch] = gv[q] + red[RV + ((nt * 2 + q) * 2 + 0) * 64 + lane];
+        o1[NT1 * COUT + ch] = gvb[q] + red[RV + ((nt * 2 + q) * 2 + 1) * 64 + lane];
+      }
     }
   }
 }
@@ -1062,7 +1392,7 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   {
     SRCNN_PROFILE("wide_prepack_w2", s);
     const int tot = 2 * NetT::W2;
-    hipLaunchKernelGGL((prepack_w2_kernel<N1, N2, F2>), dim3((tot + 255) / 256), dim3(256), 0, s,
+    hipLaunchKernelGGL((prepack_w2_kernel<N1, N2, F2, kWideD16>), dim3((tot + 255) / 256), dim3(256), 0, s,
                        W2, Wf, Wd);
     SRCNN_LAUNCH_TRY();
   }
@@ -1091,11 +1421,18 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   }
   {
     SRCNN_PROFILE("wide_delta1_grad1", s);
-    const size_t lds = (2 * ((size_t)cd.img_w * cd.img_h * kPS + kImgSlack) + 2 * kXBuf +
-                        2 * NetT::MT4 * 33) * sizeof(float);  // + the class-order pixel table
-    if (int rc = set_lds(conv_mfma_kernel<N2, N1, F2, NetT::MT4, true, F1>, lds)) return rc;
-    hipLaunchKernelGGL((conv_mfma_kernel<N2, N1, F2, NetT::MT4, true, F1>), dim3(GD), dim3(256),
-                       lds, s, D2, Wd, (const float*)nullptr, A1, (float*)nullptr, X, slab1, cd);
+    if (kWideD16) {
+      const size_t lds = (2 * ((size_t)cd.img_w * cd.img_h * kPS + kImgSlack) + 2 * kXBuf + kD16Slots +
+                          4 * kD16MT) * sizeof(float);  // + the slot -> pixel table, tile masks, tile order
+      if (int rc = set_lds(d1g16_kernel<N2, N1, F2, F1>, lds)) return rc;
+      hipLaunchKernelGGL((d1g16_kernel<N2, N1, F2, F1>), dim3(GD), dim3(256), lds, s, D2, Wd, A1, X, slab1, cd);
+    } else {
+      const size_t lds = (2 * ((size_t)cd.img_w * cd.img_h * kPS + kImgSlack) + 2 * kXBuf +
+                          2 * NetT::MT4 * 33) * sizeof(float);  // + the class-order pixel table
+      if (int rc = set_lds(conv_mfma_kernel<N2, N1, F2, NetT::MT4, true, F1>, lds)) return rc;
+      hipLaunchKernelGGL((conv_mfma_kernel<N2, N1, F2, NetT::MT4, true, F1>), dim3(GD), dim3(256),
+                         lds, s, D2, Wd, (const float*)nullptr, A1, (float*)nullptr, X, slab1, cd);
+    }
     SRCNN_LAUNCH_TRY();
   }
   {
