@@ -640,6 +640,9 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restri
 #define SRCNN_WIDE_D16 1
 #endif
 constexpr bool kWideD16 = SRCNN_WIDE_D16;
+#ifndef SRCNN_D16_MASK_AHEAD
+#define SRCNN_D16_MASK_AHEAD 3  // epilogue relu' loads run this many tiles ahead
+#endif
 constexpr int kD16MT = 20;                   // 16-pixel tiles per wave group
 constexpr int kD16Slots = 2 * kD16MT * 16;  // pixel slots of the tile table
 template <int CIN, int COUT, int F, int F1>
@@ -836,7 +839,10 @@ __global__ __launch_bounds__(256, 1) void d1g16_kernel(const float* __restrict__
     // epilogue: delta1 = relu'(A1) * acc, then gW1 += Xwin^T delta1
     const float* xs = xsm + ipar * kXBuf;
     const size_t obase = (size_t)s * g.npx * COUT + part * 64 + nt * 32 + i16;
-    float mk[2][4], mkn[2][4];
+    // relu' operands (A1, from HBM) kEpD tiles ahead in a ring of named sets:
+    // a tile's gW1 work (48 MFMAs) is shorter than one HBM round trip
+    constexpr int kEpD = SRCNN_D16_MASK_AHEAD;
+    float mk[kEpD + 1][2][4];
     auto ldmask = [&](int m, float (&d)[2][4]) {
 #pragma unroll
       for (int r = 0; r < 4; r++) {
@@ -845,15 +851,17 @@ __global__ __launch_bounds__(256, 1) void d1g16_kernel(const float* __restrict__
         for (int q = 0; q < 2; q++) d[q][r] = ycur[obase + (size_t)pix * COUT + 16 * q];
       }
     };
-    ldmask(0, mk);
+#pragma unroll
+    for (int m = 0; m < kEpD; m++) ldmask(m, mk[m]);
 #pragma unroll
     for (int m = 0; m < MT; m++) {
-      if (m + 1 < MT) ldmask(m + 1, mkn);
+      if (m + kEpD < MT) ldmask(m + kEpD, mk[(m + kEpD) % (kEpD + 1)]);
       const int s0 = tbase[m] + 4 * g4;
 #pragma unroll
       for (int r = 0; r < 4; r++)
 #pragma unroll
-        for (int q = 0; q < 2; q++) acc[m][q][r] = (s0 + r < g.npx && mk[q][r] > 0.0f) ? acc[m][q][r] : 0.0f;
+        for (int q = 0; q < 2; q++)
+          acc[m][q][r] = (s0 + r < g.npx && mk[m % (kEpD + 1)][q][r] > 0.0f) ? acc[m][q][r] : 0.0f;
       // X windows of k-step r (pixel slot s0 + r), one k-step ahead, two named sets
       float xq[2][TT + 1];
       auto xrd = [&](int r) {
@@ -878,12 +886,6 @@ __global__ __launch_bounds__(256, 1) void d1g16_kernel(const float* __restrict__
           gvb[q] += acc[m][q][r];
         }
         __builtin_amdgcn_sched_barrier(0);
-      }
-      if (m + 1 < MT) {
-#pragma unroll
-        for (int q = 0; q < 2; q++)
-#pragma unroll
-          for (int r = 0; r < 4; r++) mk[q][r] = mkn[q][r];
       }
     }
   }
