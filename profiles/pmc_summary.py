@@ -29,6 +29,7 @@ SHORT = [
     (r"wide::wl1_fwd_kernel", "wide_l1_fwd"),
     (r"wide::conv_mfma_kernel<128, 64", "wide_l2_fwd"),
     (r"wide::conv_mfma_kernel<64, 128", "wide_delta1_grad1"),
+    (r"wide::d1g16_kernel", "wide_delta1_grad1"),
     (r"wide::wl3_kernel", "wide_l3_delta"),
     (r"wide::wgrad2_kernel", "wide_grad2"),
     (r"sgd_update_kernel", "sgd_update"),
