@@ -1145,6 +1145,189 @@ __global__ __launch_bounds__(256, 2) void wl3_kernel(const float* __restrict__ A
 }
 
 // ---------------------------------------------------------------------------
+// wl3l: wl3 with the sample's A2 resident in LDS (round 3).  The Q phase
+// writes the A2 operands it loaded into a quad-swizzled LDS image, so the
+// delta2 mask and gW3's operand come from LDS and A2 is read from HBM once
+// (wl3 read it twice: 1.51x the fused-minimum bytes).  A2 (441 x 64 floats,
+// 112.9 KB) + Q (44.1 KB) + the delta3 grid fill the LDS, so one block of 8
+// waves per CU; the next sample's first Q tile is loaded before the delta2
+// stores (a store counts in vmcnt too) and lands under delta2 / gW3.
+// ---------------------------------------------------------------------------
+#ifndef SRCNN_WL3_LDS
+#define SRCNN_WL3_LDS 1
+#endif
+constexpr bool kWl3Lds = SRCNN_WL3_LDS;
+template <int N2>
+__device__ __forceinline__ int wl3l_at(int p, int c) {  // A2 image float index, quads XOR-swizzled by pixel
+  return p * N2 + 4 * ((c >> 2) ^ (p & (N2 / 4 - 1))) + (c & 3);
+}
+template <int N2, int F3>
+__global__ __launch_bounds__(512, 1) void wl3l_kernel(const float* __restrict__ A2,
+                                                     const float* __restrict__ T,
+                                                     const float* __restrict__ W3,
+                                                     const float* __restrict__ B3,
+                                                     float* __restrict__ D2, float* __restrict__ slab3,
+                                                     float* __restrict__ sqs, float* __restrict__ A3out,
+                                                     WGeom g) {
+  static_assert(N2 == 64 && F3 * F3 <= 32, "shape");
+  constexpr int FF = F3 * F3, KP3 = (FF + 1) / 2, P3 = FF * N2 + 1, NW = 8;
+  extern __shared__ float smem[];
+  const int npx2 = g.w2 * g.h2, mt2 = (npx2 + 31) / 32, npx3 = g.w3 * g.h3;
+  const int GW = g.w3 + 2 * (F3 - 1), GH = g.h3 + 2 * (F3 - 1);
+  float* a2i = smem;                  // [npx2][N2], swizzled; the end-of-kernel reduction
+  float* Qs = smem + npx2 * N2;       // [npx2][FF]
+  float* Gd = Qs + npx2 * FF;         // [GH][GW]
+  __shared__ float red_s[2][NW];
+  const int lane = lane_id(), wave = wave_id(), j = lane & 31, h = lane >> 5;
+  const int padT = (g.w - g.w3) / 2;  // last_layer_delta.cl:25 (from the width)
+  for (int i = threadIdx.x; i < GW * GH; i += 512) Gd[i] = 0.0f;
+  float wq[8][4];
+#pragma unroll
+  for (int kk = 0; kk < 8; kk++)
+#pragma unroll
+    for (int jj = 0; jj < 4; jj++) wq[kk][jj] = j < FF ? W3[j * N2 + 8 * kk + 4 * h + jj] : 0.0f;
+  const int nt = wave & 1, mg = wave >> 1;  // delta2: N tile, M group (4)
+  float wd[KP3];
+  int goff[KP3];
+#pragma unroll
+  for (int kp = 0; kp < KP3; kp++) {
+    const int t = kp + KP3 * h, tc = min(t, FF - 1);
+    wd[kp] = t < FF ? W3[t * N2 + 32 * nt + j] : 0.0f;
+    goff[kp] = -((tc / F3) * GW + tc % F3);
+  }
+  const int tA = min(j, FF - 1);
+  const int goffA = -((tA / F3) * GW + tA % F3);
+  const bool tapA = j < FF;
+  f32x16 gacc0 = zero16(), gacc1 = zero16();
+  float sq = 0.0f, gb3 = 0.0f;
+  const float b3 = B3[0];
+  float4 vn[8];
+  auto ldq = [&](const float* a2s_, int mt_) {
+    const int p = min(32 * mt_ + j, npx2 - 1);
+    const float4* src = reinterpret_cast<const float4*>(a2s_ + (size_t)p * N2) + h;
+#pragma unroll
+    for (int kk = 0; kk < 8; kk++) vn[kk] = src[2 * kk];
+  };
+  if ((int)blockIdx.x < g.batch && wave < mt2) ldq(A2 + (size_t)blockIdx.x * npx2 * N2, wave);
+  for (int s = blockIdx.x; s < g.batch; s += gridDim.x) {
+    const float* a2s = A2 + (size_t)s * npx2 * N2;
+    const float* ts = T + (size_t)s * g.w * g.h;
+    __syncthreads();  // the previous sample's readers of every LDS region are done
+    float tv = 0.0f;  // this thread's target pixel (outputs past 512: loaded in place)
+    {
+      const int o = min((int)threadIdx.x, npx3 - 1), oy = o / g.w3, ox = o - oy * g.w3;
+      tv = ts[(oy + padT) * g.w + ox + padT];
+    }
+    // 1. Q, and the A2 image
+    for (int mt = wave; mt < mt2; mt += NW) {
+      float4 v[8];
+#pragma unroll
+      for (int kk = 0; kk < 8; kk++) v[kk] = vn[kk];
+      if (mt + NW < mt2) ldq(a2s, mt + NW);
+      f32x16 acc = zero16();
+#pragma unroll
+      for (int kk = 0; kk < 8; kk++)
+#pragma unroll
+        for (int jj = 0; jj < 4; jj++) acc = mma(v[kk][jj], wq[kk][jj], acc);
+      const int p = 32 * mt + j;
+      if (p < npx2)
+#pragma unroll
+        for (int kk = 0; kk < 8; kk++) *reinterpret_cast<float4*>(a2i + wl3l_at<N2>(p, 8 * kk + 4 * h)) = v[kk];
+#pragma unroll
+      for (int r = 0; r < 16; r++) {
+        const int pix = 32 * mt + crow(r, h);
+        if (pix < npx2 && j < FF) Qs[pix * FF + j] = acc[r];
+      }
+    }
+    __syncthreads();
+    // 2. A3, last delta, squared error
+    for (int o = threadIdx.x; o < npx3; o += 512) {
+      const int oy = o / g.w3, ox = o - oy * g.w3;
+      const float* q0 = Qs + (oy * g.w2 + ox) * FF;
+      float v = 0.0f;
+#pragma unroll
+      for (int t = 0; t < FF; t++) v += q0[((t / F3) * g.w2 + t % F3) * FF + t];
+      const float a3 = v + b3;
+      A3out[(size_t)s * npx3 + o] = a3;  // to the workspace (srcnn_train_activations)
+      const float tgt = o == (int)threadIdx.x ? tv : ts[(oy + padT) * g.w + ox + padT];
+      const float diff = a3 - tgt;
+      const float d = a3 > 0.0f ? diff : 0.0f;
+      sq += diff * diff;
+      gb3 += d;
+      Gd[(oy + F3 - 1) * GW + ox + F3 - 1] = d;
+    }
+    __syncthreads();
+    // the next sample's first Q tile, issued before the delta2 stores
+    if (s + (int)gridDim.x < g.batch && wave < mt2) ldq(a2s + (size_t)gridDim.x * npx2 * N2, wave);
+    // 3. delta2 = [A2 > 0] sum_t Gd W3 (channel 32 nt + j)
+    const int mc = 32 * nt + j;
+    for (int mt = mg; mt < mt2; mt += NW / 2) {
+      const int p = min(32 * mt + j, npx2 - 1), py = p / g.w2, px = p - py * g.w2;
+      const int gb = (py + F3 - 1) * GW + px + F3 - 1;
+      f32x16 acc = zero16();
+#pragma unroll
+      for (int kp = 0; kp < KP3; kp++) acc = mma(Gd[gb + goff[kp]], wd[kp], acc);
+#pragma unroll
+      for (int r = 0; r < 16; r++) {
+        const int pix = 32 * mt + crow(r, h);
+        if (pix < npx2) {
+          const size_t idx = ((size_t)s * npx2 + pix) * N2 + mc;
+          D2[idx] = a2i[wl3l_at<N2>(pix, mc)] > 0.0f ? acc[r] : 0.0f;
+        }
+      }
+    }
+    // 4. gW3 (K = pixel pairs kp = wave + NW i; B columns: channel 2j + tile);
+    // batching the LDS reads of 4 or 8 pairs ahead of their MFMAs measured
+    // slower (0.349 / 0.356 vs 0.341 ms)
+    for (int kp = wave; 2 * kp < npx2; kp += NW) {
+      const int pk = 2 * kp + h;
+      const bool pok = pk < npx2;
+      const int p = pok ? pk : npx2 - 1, py = p / g.w2, px = p - py * g.w2;
+      const float av = Gd[(py + F3 - 1) * GW + px + F3 - 1 + goffA];
+      const float a = (tapA && pok) ? av : 0.0f;
+      const float2 bv = *reinterpret_cast<const float2*>(a2i + wl3l_at<N2>(p, 2 * j));
+      gacc0 = mma(a, bv.x, gacc0);
+      gacc1 = mma(a, bv.y, gacc1);
+    }
+  }
+  // cross-wave reduction of gW3 (fixed wave order), gB3, squared error
+  __syncthreads();
+  float* red = a2i;  // NW waves x 2 tiles x 16 regs x 64 lanes
+#pragma unroll
+  for (int r = 0; r < 16; r++) {
+    red[((wave * 2 + 0) * 16 + r) * 64 + lane] = gacc0[r];
+    red[((wave * 2 + 1) * 16 + r) * 64 + lane] = gacc1[r];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    sq += __shfl_down(sq, o, 64);
+    gb3 += __shfl_down(gb3, o, 64);
+  }
+  if (lane == 0) {
+    red_s[0][wave] = sq;
+    red_s[1][wave] = gb3;
+  }
+  __syncthreads();
+  float* out = slab3 + (size_t)blockIdx.x * P3;
+  for (int e = threadIdx.x; e < 2 * 16 * 64; e += 512) {
+    const int tile = e / (16 * 64), r = (e / 64) % 16, l = e & 63;
+    const int tap = crow(r, l >> 5), c = 2 * (l & 31) + tile;
+    float v = 0.0f;
+    for (int w = 0; w < NW; w++) v += red[((w * 2 + tile) * 16 + r) * 64 + l];
+    if (tap < FF) out[tap * N2 + c] = v;
+  }
+  if (threadIdx.x == 0) {
+    float b = 0.0f, q = 0.0f;
+    for (int w = 0; w < NW; w++) {
+      b += red_s[1][w];
+      q += red_s[0][w];
+    }
+    out[FF * N2] = b;
+    sqs[blockIdx.x] = q;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // wgrad2: gW2[t][c][n] += sum_{s,p} A1[p + off(t)][c] delta2[p][n]; gB2[n] += sum delta2
 // (backpropagate.cl:64-113, summed race-free).  16x16x4 MFMA: rows = 16
 // channels, cols = 16 n, K = 4 pixels.  Block = (32-channel chunk cq, sample
@@ -1362,10 +1545,13 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   const int qfloats = std::max(npx2 * F3 * F3, 2 * 16 * 64 * 4);
   const size_t lds3 = (size_t)(qfloats + (g.w3 + 2 * (F3 - 1)) * (g.h3 + 2 * (F3 - 1)) + 2 * npx2) * 4;
   if (lds3 > 64 * 1024) return 0;
+  // wl3l: A2 image + Q + delta3 grid (the reduction reuses the A2 image)
+  const size_t lds3l = (size_t)(npx2 * N2 + npx2 * F3 * F3 + (g.w3 + 2 * (F3 - 1)) * (g.h3 + 2 * (F3 - 1))) * 4;
+  const bool wl3l = kWl3Lds && lds3l <= 160 * 1024 && npx2 * N2 >= 2 * 16 * 64 * 8 && g.w3 * g.h3 <= 512;
   constexpr int NPD = N1 / 64;  // delta1 items per sample (64-channel parts)
   const int GD = std::min(g.batch * NPD, 256);  // a multiple of NPD: block parity = part
   const int G1 = GD / NPD;                      // gW1 slabs: one per block pair
-  const int G3 = (int)std::min<uint32_t>(batch, 512);
+  const int G3 = (int)std::min<uint32_t>(batch, wl3l ? 256 : 512);  // all blocks resident
   const int GC = 256;
   const int G2 = g2.groups * (N1 / 32);
   // workspace: Wf | Wd | slab1 | slab2 | slab3 | sqs
@@ -1416,9 +1602,15 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   }
   {
     SRCNN_PROFILE("wide_l3_delta", s);
-    if (int rc = set_lds(wl3_kernel<N2, F3>, lds3)) return rc;
-    hipLaunchKernelGGL((wl3_kernel<N2, F3>), dim3(G3), dim3(256), lds3, s, A2, T, W3, B3, D2,
-                       slab3, sqs, A3, g, qfloats);
+    if (wl3l) {
+      if (int rc = set_lds(wl3l_kernel<N2, F3>, lds3l)) return rc;
+      hipLaunchKernelGGL((wl3l_kernel<N2, F3>), dim3(G3), dim3(512), lds3l, s, A2, T, W3, B3, D2, slab3, sqs,
+                         A3, g);
+    } else {
+      if (int rc = set_lds(wl3_kernel<N2, F3>, lds3)) return rc;
+      hipLaunchKernelGGL((wl3_kernel<N2, F3>), dim3(G3), dim3(256), lds3, s, A2, T, W3, B3, D2,
+                         slab3, sqs, A3, g, qfloats);
+    }
     SRCNN_LAUNCH_TRY();
   }
   {
