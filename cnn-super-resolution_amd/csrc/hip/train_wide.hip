@@ -689,7 +689,7 @@ __global__ __launch_bounds__(256, 1) void d1g16_kernel(const float* __restrict__
   if (threadIdx.x == 0) {
     constexpr int B = F - 1;
     int n = 0;
-    if (ow < 2 * B + 1 || oh < 2 * B + 1) {
+    if (ow < 2 * B + 1 || oh < 2 * B + 1 || ow * oh > kD16Slots) {  // (the host keeps ow * oh <= kD16Slots)
       for (; n < ow * oh && n < kD16Slots; n++) ptab[n] = n;  // raster order
     } else {
       auto lo = [&](int c, int e) { return c < B ? c : (c == B ? B : e - 2 * B - 1 + c); };
