@@ -31,6 +31,7 @@ SHORT = [
     (r"wide::conv_mfma_kernel<64, 128", "wide_delta1_grad1"),
     (r"wide::d1g16_kernel", "wide_delta1_grad1"),
     (r"wide::wl3_kernel", "wide_l3_delta"),
+    (r"wide::wl3l_kernel", "wide_l3_delta"),
     (r"wide::wgrad2_kernel", "wide_grad2"),
     (r"sgd_update_kernel", "sgd_update"),
     (r"update_all_kernel", "update_all"),
