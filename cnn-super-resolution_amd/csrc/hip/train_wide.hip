@@ -802,7 +802,7 @@ __global__ __launch_bounds__(256, 1) void d1g16_kernel(const float* __restrict__
 #pragma unroll
           for (int q = 0; q < 2; q++) bq[(dx + F - 1) % F][q] = wp[(size_t)q * WQ + kb * 64];
           // the next chunk's whole DMA in the first tap, after its B loads (conv_mfma)
-          if (t == 0 && stage)
+          if (t == 0 && stage && !(kWDiag & 4))
             for (int k = wave; k < kdma; k += 4) dma(nit / NP, nc, nxt, k);
           // tiles MH.. of tap t load while tiles ..MH of tap t run
 #pragma unroll
