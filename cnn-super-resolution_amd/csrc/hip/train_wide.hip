@@ -218,6 +218,15 @@ __global__ void prepack_w2_kernel(const float* __restrict__ W2, float* __restric
 // the DMA instructions go out as one burst in the chunk's first tap, after
 // that tap's B loads, so only the B waits of tap 4 cover them.
 // ---------------------------------------------------------------------------
+// the next chunk's LDS-DMA in kDmaSplit bursts, at taps 0, kDmaEvery, ...
+#ifndef SRCNN_WIDE_DMA_SPLIT
+#define SRCNN_WIDE_DMA_SPLIT 1
+#endif
+#ifndef SRCNN_WIDE_DMA_EVERY
+#define SRCNN_WIDE_DMA_EVERY 8
+#endif
+constexpr int kDmaSplit = SRCNN_WIDE_DMA_SPLIT, kDmaEvery = SRCNN_WIDE_DMA_EVERY;
+static_assert(kDmaSplit >= 1 && (kDmaSplit - 1) * kDmaEvery < 25, "DMA bursts within the chunk's taps");
 constexpr int kImgMax = 960;                  // pixels of one chunk image (<= 31 x 31)
 constexpr int kImgSlack = 256;                // floats: one DMA instruction past the image
 
@@ -389,14 +398,18 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restri
   // the image pixel of M-tile slot `slot` (raster order unless G1)
   auto pix_of = [&](int slot, int npxw_) { return G1 ? ptab[slot] : min(slot, npxw_ - 1); };
   // one LDS-DMA instruction k (64 slots of 16 B) of chunk c of window wn
+  // (every window's image is img_w wide: pix / img_w as a multiply, exact for
+  // pix < 4096; the predicate is formed without short-circuit branches)
+  const uint32_t iw_mag = (1u << 20) / (uint32_t)g.img_w + 1u;
   auto dma = [&](const CWin& wn, int c, float* buf, int k) {
     const int slot = k * 64 + lane;
     const int pix = slot / 5, q = slot - 5 * pix;
-    const int iy = pix / wn.iw, ix = pix - iy * wn.iw;
+    const int iy = (int)(((uint32_t)pix * iw_mag) >> 20), ix = pix - iy * wn.iw;
     const int y = wn.y0 + iy - g.pad, x = wn.x0 + ix - g.pad;
-    const bool ok = q < 4 && slot < wn.iw * wn.ih * 5 && y >= 0 && y < g.in_h && x >= 0 && x < g.in_w;
-    const float* src =
-        ok ? in + ((size_t)(wn.s * g.in_h + y) * g.in_w + x) * CIN + c * kCC + 4 * q : g_zero_src;
+    const bool ok = (q < 4) & (slot < wn.iw * wn.ih * 5) & ((unsigned)y < (unsigned)g.in_h) &
+                    ((unsigned)x < (unsigned)g.in_w);
+    const float* base = in + ((size_t)wn.s * g.in_h * g.in_w) * CIN + c * kCC;
+    const float* src = ok ? base + (y * g.in_w + x) * CIN + 4 * q : g_zero_src;
     dma16(src, buf + k * 256);
   };
   auto kdma_of = [](const CWin& wn) { return (wn.iw * wn.ih * 5 + 63) / 64; };
@@ -470,8 +483,11 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restri
           // taps (2 per tap), the DMAs were waited on 3 taps after issue; as
           // one burst at tap 0 only the B loads of tap 4 wait for them
           // (same-box A/B: delta1 + gW1 -1.0%, L2 forward -1.0%)
-          if (t == 0 && stage && !(kWDiag & 4))
-            for (int k = wave; k < kdma; k += 4) dma(wd, nc, nxt, k);
+          if (stage && !(kWDiag & 4) && t % kDmaEvery == 0 && t / kDmaEvery < kDmaSplit) {
+            const int part_ = t / kDmaEvery, lo = kdma * part_ / kDmaSplit, hi = kdma * (part_ + 1) / kDmaSplit;
+            for (int k = wave; k < kdma; k += 4)
+              if (k >= lo && k < hi) dma(wd, nc, nxt, k);
+          }
           // k-step (t, 0) while (t, 1) loads; k-step (t, 1) while (t + 1, 0)
           // loads.  sched_barriers pin the order: left alone, the scheduler
           // sinks the prefetch reads below the MFMAs and exposes LDS latency.
@@ -746,13 +762,17 @@ __global__ __launch_bounds__(256, 1) void d1g16_kernel(const float* __restrict__
     const int o = ptab[16 * T + i16], oy = o / ow;
     abase[m] = (oy * g.img_w + o - oy * ow) * kPS + 4 * g4;
   }
+  // pix / img_w as a multiply (exact for pix < 4096), predicate without branches
+  const uint32_t iw_mag = (1u << 20) / (uint32_t)g.img_w + 1u;
   auto dma = [&](int s, int c, float* buf, int k) {
     const int slot = k * 64 + lane;
     const int pix = slot / 5, q = slot - 5 * pix;
-    const int iy = pix / g.img_w, ix = pix - iy * g.img_w;
+    const int iy = (int)(((uint32_t)pix * iw_mag) >> 20), ix = pix - iy * g.img_w;
     const int y = iy - g.pad, x = ix - g.pad;
-    const bool ok = q < 4 && slot < g.img_w * g.img_h * 5 && y >= 0 && y < g.in_h && x >= 0 && x < g.in_w;
-    const float* src = ok ? in + ((size_t)(s * g.in_h + y) * g.in_w + x) * CIN + c * kCC + 4 * q : g_zero_src;
+    const bool ok = (q < 4) & (slot < g.img_w * g.img_h * 5) & ((unsigned)y < (unsigned)g.in_h) &
+                    ((unsigned)x < (unsigned)g.in_w);
+    const float* base = in + ((size_t)s * g.in_h * g.in_w) * CIN + c * kCC;
+    const float* src = ok ? base + (y * g.in_w + x) * CIN + 4 * q : g_zero_src;
     dma16(src, buf + k * 256);
   };
   const int kdma = (g.img_w * g.img_h * 5 + 63) / 64;
@@ -802,8 +822,11 @@ __global__ __launch_bounds__(256, 1) void d1g16_kernel(const float* __restrict__
 #pragma unroll
           for (int q = 0; q < 2; q++) bq[(dx + F - 1) % F][q] = wp[(size_t)q * WQ + kb * 64];
           // the next chunk's whole DMA in the first tap, after its B loads (conv_mfma)
-          if (t == 0 && stage && !(kWDiag & 4))
-            for (int k = wave; k < kdma; k += 4) dma(nit / NP, nc, nxt, k);
+          if (stage && !(kWDiag & 4) && t % kDmaEvery == 0 && t / kDmaEvery < kDmaSplit) {
+            const int part_ = t / kDmaEvery, lo = kdma * part_ / kDmaSplit, hi = kdma * (part_ + 1) / kDmaSplit;
+            for (int k = wave; k < kdma; k += 4)
+              if (k >= lo && k < hi) dma(nit / NP, nc, nxt, k);
+          }
           // tiles MH.. of tap t load while tiles ..MH of tap t run
 #pragma unroll
           for (int m = 0; m < MH; m++) an[m] = *reinterpret_cast<const float4*>(cur + abase[MH + m] + toff);
