@@ -861,6 +861,7 @@ __global__ __launch_bounds__(256, 1) void d1g16_kernel(const float* __restrict__
     }
     // epilogue: delta1 = relu'(A1) * acc, then gW1 += Xwin^T delta1
     const float* xs = xsm + ipar * kXBuf;
+    const uint32_t ow_mag = (1u << 20) / (uint32_t)ow + 1u;  // pix / ow as a multiply (pix < 4096)
     const size_t obase = (size_t)s * g.npx * COUT + part * 64 + nt * 32 + i16;
     // relu' operands (A1, from HBM) kEpD tiles ahead in a ring of named sets:
     // a tile's gW1 work (48 MFMAs) is shorter than one HBM round trip
@@ -888,7 +889,7 @@ __global__ __launch_bounds__(256, 1) void d1g16_kernel(const float* __restrict__
       // X windows of k-step r (pixel slot s0 + r), one k-step ahead, two named sets
       float xq[2][TT + 1];
       auto xrd = [&](int r) {
-        const int pix = ptab[s0 + r], py = pix / ow;
+        const int pix = ptab[s0 + r], py = (int)(((uint32_t)pix * ow_mag) >> 20);
         const int xb = py * kXS + pix - py * ow;
 #pragma unroll
         for (int tt = 0; tt < TT; tt++) xq[r & 1][tt] = xs[xb + toffx[tt]];
@@ -1000,6 +1001,8 @@ __global__ __launch_bounds__(256, 2) void wl3_kernel(const float* __restrict__ A
   const int npx2 = g.w2 * g.h2, mt2 = (npx2 + 31) / 32, npx3 = g.w3 * g.h3;
   const int GW = g.w3 + 2 * (F3 - 1), GH = g.h3 + 2 * (F3 - 1);
   const int padT = (g.w - g.w3) / 2;  // last_layer_delta.cl:25 (from the width)
+  const uint32_t w2_mag = (1u << 20) / (uint32_t)g.w2 + 1u;  // p / w2 as a multiply (p < 4096)
+  auto row_of = [&](int p) { return (int)(((uint32_t)p * w2_mag) >> 20); };
   for (int i = threadIdx.x; i < GW * GH; i += 256) Gd[i] = 0.0f;
   // step 1 B operand: W3[t = j][c = 8kk + 4h + jj]
   float wq[8][4];
@@ -1084,7 +1087,7 @@ __global__ __launch_bounds__(256, 2) void wl3_kernel(const float* __restrict__ A
     // 3. delta2 (channel 32nt + j: mask word half mh, bit mbit)
     const int mc = 32 * nt + j, mh = (mc >> 2) & 1, mbit = 4 * (mc >> 3) + (mc & 3);
     for (int mt = mg; mt < mt2; mt += 2) {
-      const int p = min(32 * mt + j, npx2 - 1), py = p / g.w2, px = p - py * g.w2;
+      const int p = min(32 * mt + j, npx2 - 1), py = row_of(p), px = p - py * g.w2;
       const int gb = (py + F3 - 1) * GW + px + F3 - 1;
       f32x16 acc = zero16();
 #pragma unroll
@@ -1112,7 +1115,7 @@ __global__ __launch_bounds__(256, 2) void wl3_kernel(const float* __restrict__ A
       for (int u = 0; u < kWl3B; u++) {
         const int pk = 2 * (wave + 4 * (i0 + u)) + h;
         const bool pok = pk < npx2;
-        const int p = pok ? pk : npx2 - 1, py = p / g.w2, px = p - py * g.w2;
+        const int p = pok ? pk : npx2 - 1, py = row_of(p), px = p - py * g.w2;
         const float av = Gd[(py + F3 - 1) * GW + px + F3 - 1 + goffA];
         a_[u] = (tapA && pok) ? av : 0.0f;
         b_[u] = *reinterpret_cast<const float2*>(a2s + (size_t)p * N2 + 2 * j);
@@ -1203,6 +1206,10 @@ __global__ __launch_bounds__(512, 1) void wl3l_kernel(const float* __restrict__ 
   __shared__ float red_s[2][NW];
   const int lane = lane_id(), wave = wave_id(), j = lane & 31, h = lane >> 5;
   const int padT = (g.w - g.w3) / 2;  // last_layer_delta.cl:25 (from the width)
+  // p / w2 as a multiply by a 20-bit reciprocal (exact for p < 4096; a runtime
+  // division costs ~15 VALU per pixel pair in the gW3 loop)
+  const uint32_t w2_mag = (1u << 20) / (uint32_t)g.w2 + 1u;
+  auto row_of = [&](int p) { return (int)(((uint32_t)p * w2_mag) >> 20); };
   for (int i = threadIdx.x; i < GW * GH; i += 512) Gd[i] = 0.0f;
   float wq[8][4];
 #pragma unroll
@@ -1285,7 +1292,7 @@ __global__ __launch_bounds__(512, 1) void wl3l_kernel(const float* __restrict__ 
     // 3. delta2 = [A2 > 0] sum_t Gd W3 (channel 32 nt + j)
     const int mc = 32 * nt + j;
     for (int mt = mg; mt < mt2; mt += NW / 2) {
-      const int p = min(32 * mt + j, npx2 - 1), py = p / g.w2, px = p - py * g.w2;
+      const int p = min(32 * mt + j, npx2 - 1), py = row_of(p), px = p - py * g.w2;
       const int gb = (py + F3 - 1) * GW + px + F3 - 1;
       f32x16 acc = zero16();
 #pragma unroll
@@ -1305,7 +1312,7 @@ __global__ __launch_bounds__(512, 1) void wl3l_kernel(const float* __restrict__ 
     for (int kp = wave; 2 * kp < npx2; kp += NW) {
       const int pk = 2 * kp + h;
       const bool pok = pk < npx2;
-      const int p = pok ? pk : npx2 - 1, py = p / g.w2, px = p - py * g.w2;
+      const int p = pok ? pk : npx2 - 1, py = row_of(p), px = p - py * g.w2;
       const float av = Gd[(py + F3 - 1) * GW + px + F3 - 1 + goffA];
       const float a = (tapA && pok) ? av : 0.0f;
       const float2 bv = *reinterpret_cast<const float2*>(a2i + wl3l_at<N2>(p, 2 * j));
