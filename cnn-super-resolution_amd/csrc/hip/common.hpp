@@ -78,6 +78,22 @@ struct Scope {
 // per-kernel slot of a device array; srcnn_profile_clock() reports their
 // median ratio.  The production kernels carry no probe.
 namespace srcnn {
+// s_waitcnt vmcnt(0) that the compiler's wait-count pass sees (expcnt and
+// lgkmcnt left at their maxima; gfx9 encoding vmcnt[3:0] | expcnt[6:4] |
+// lgkmcnt[11:8] | vmcnt[5:4] << 14).  The kernels issue their LDS-DMA as
+// inline asm, which that pass cannot count; after an inline-asm vmcnt(0) it
+// still believed older loads outstanding and, at their first use, emitted a
+// vmcnt(N) that waited for the DMA just issued.  After this one it knows them
+// complete and emits no such wait.
+#ifndef SRCNN_VISIBLE_WAIT
+#define SRCNN_VISIBLE_WAIT 1
+#endif
+__device__ __forceinline__ void wait_vm0() {
+  if (SRCNN_VISIBLE_WAIT)
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+  else
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
 constexpr int kClockBlocks = 8;
 #ifdef SRCNN_CLOCK_PROBE
 constexpr bool kClockProbe = true;

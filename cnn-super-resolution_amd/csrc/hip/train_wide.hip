@@ -419,7 +419,7 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restri
     const CWin w0 = conv_win<F, NP>(blockIdx.x, g);
     for (int k = wave; k < kdma_of(w0); k += 4) dma(w0, 0, buf0, k);
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  wait_vm0();
   __syncthreads();
   int bsel = 0, ipar = 0;
   for (int it = blockIdx.x; it < nitems; it += gridDim.x, ipar ^= 1) {
@@ -515,7 +515,7 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restri
           __builtin_amdgcn_sched_barrier(0);
         }
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      wait_vm0();
       __syncthreads();
       bsel ^= 1;
     }
@@ -780,7 +780,7 @@ __global__ __launch_bounds__(256, 1) void d1g16_kernel(const float* __restrict__
   float* const buf1 = smem + buf_floats;
   if ((int)blockIdx.x < nitems)
     for (int k = wave; k < kdma; k += 4) dma(blockIdx.x / NP, 0, buf0, k);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  wait_vm0();
   __syncthreads();
   int bsel = 0, ipar = 0;
   for (int it = blockIdx.x; it < nitems; it += gridDim.x, ipar ^= 1) {
@@ -855,7 +855,7 @@ __global__ __launch_bounds__(256, 1) void d1g16_kernel(const float* __restrict__
           __builtin_amdgcn_sched_barrier(0);
         }
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      wait_vm0();
       __syncthreads();
       bsel ^= 1;
     }
@@ -1462,7 +1462,7 @@ __global__ __launch_bounds__(512, 1) void wgrad2_kernel(const float* __restrict_
   int bsel = 0;
   if (nunits > 0) stage(0, smem);
   for (int u = 0; u < nunits; u++) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    wait_vm0();
     if (!(kWg2Diag & 4) || u == 0) __syncthreads();  // unit u landed; everyone is done with the other buffer
     const float* cur = smem + (bsel ? kGBuf : 0);
     if (u + 1 < nunits && !(kWg2Diag & 2)) stage(u + 1, smem + (bsel ? 0 : kGBuf));
