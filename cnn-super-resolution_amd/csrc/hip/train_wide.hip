@@ -581,6 +581,7 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restri
       }
     } else {
       const float bn = DELTA ? 0.0f : bias[n];
+      const uint32_t ow_mag = (1u << 20) / (uint32_t)cw.ow + 1u;  // exact for pix < 4096
       // one 32-pixel tile at a time; the lane index is made opaque per tile so
       // the compiler cannot hoist all 16*MT store addresses out of the item loop
 #pragma unroll
@@ -592,7 +593,9 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restri
         for (int r = 0; r < 16; r++) {
           const int pix = p0 + crow(r, 0);
           if (pix < npxw) {
-            const int py = cw.ow == g.out_w ? 0 : pix / cw.ow;  // window pixel -> image pixel
+            // window pixel -> image pixel (row by a reciprocal multiply; 0 for
+            // full-width windows, where the runtime division used to run anyway)
+            const int py = cw.ow == g.out_w ? 0 : (int)(((uint32_t)pix * ow_mag) >> 20);
             const size_t idx = obase + (size_t)(pix + py * (g.out_w - cw.ow)) * COUT;
             if (DELTA)
               out[idx] = ycur[idx] > 0.0f ? acc[m][r] : 0.0f;
