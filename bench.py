@@ -13,13 +13,20 @@ through its C ABI); inputs are resident in HBM before the timed region.
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
-Rank 0 prints ONE JSON line.  Data is synthetic (smooth random luma patches,
-seed 1234 + rank; weights N(0, 1e-3), biases 0).
+`--gpus N > 1` without a torch.distributed.run environment launches the N
+rank processes itself (torch.distributed.run as a child process, before any
+GPU call) and exits with its status; under torch.distributed.run, WORLD_SIZE
+must equal --gpus.  Rank 0 prints ONE JSON line.  With N > 1 the line also
+carries the strong-scaling step (global batch 4096 sharded over the ranks)
+under "strong".  Data is synthetic (smooth random luma patches, seed
+1234 + rank; weights N(0, 1e-3), biases 0).
 """
 import argparse
 import glob
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -243,6 +250,14 @@ def host_cores():
     return avail, want
 
 
+def threads_source():
+    """Where the CPU baseline's thread count comes from (reported beside it)."""
+    if os.environ.get("OMP_NUM_THREADS"):
+        return ("OMP_NUM_THREADS=%s (the host's per-GPU CPU share on the GPU box; the other "
+                "host CPUs belong to the other GPUs' jobs)" % os.environ["OMP_NUM_THREADS"])
+    return "every CPU of the affinity mask"
+
+
 def cpu_baseline(net, tiles_min=16, budget_s=12.0):
     """Time the CPU restatement of the reference path (oracle/, OpenMP) on a
     bounded sample of the same workload."""
@@ -267,6 +282,7 @@ def cpu_baseline(net, tiles_min=16, budget_s=12.0):
         if el >= budget_s:
             break
     return {"value": round(done / el, 2), "unit": "tiles/s", "cores": threads, "host_cpus": avail,
+            "cores_from": threads_source(),
             "kind": "port",
             "sample": "%d tiles of 33x33 (default net, fwd+bwd+update) in %.1fs with the oracle C "
                       "restatement (oracle/srcnn_oracle.c), OpenMP over tiles" % (done, el)}
@@ -291,7 +307,7 @@ def cpu_forward_baseline(net, strip_rows=256, reps=3):
     threads = orc.set_threads(want)
     prm = init_params(net, orc.param_count(*net))
     rng = np.random.default_rng(5)
-    out = {"cores": threads, "host_cpus": avail, "kind": "port"}
+    out = {"cores": threads, "host_cpus": avail, "cores_from": threads_source(), "kind": "port"}
     x = (rng.random(256 * 256, dtype=np.float32) - 0.5)
     orc.forward(net, x, 256, 256, 1, prm)
     ts = []
@@ -503,9 +519,132 @@ def _mark(what):
         print("[bench %.1f ms] %s" % ((time.perf_counter() - _T0) * 1e3, what), file=sys.stderr, flush=True)
 
 
+STRONG_GLOBAL_BATCH = 4096  # strong scaling over a 4096-tile global batch
+
+
+def launch_plan(gpus, env):
+    """How this invocation runs (reference training loop: Main_cl.cpp:161-195,
+    one process per GPU here).  Returns ("run", world) when this process is
+    one rank already -- WORLD_SIZE from torch.distributed.run, or a single
+    GPU -- and ("spawn", gpus) when --gpus N > 1 was asked for without a
+    launcher, so the N ranks must be started first.  A WORLD_SIZE that
+    disagrees with --gpus is an error (the line would be mislabelled)."""
+    if gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1 (got %d)" % gpus)
+    ws = env.get("WORLD_SIZE")
+    if ws is None or ws == "":
+        return ("spawn", gpus) if gpus > 1 else ("run", 1)
+    try:
+        world = int(ws)
+    except ValueError:
+        raise SystemExit("bench.py: WORLD_SIZE=%r is not an integer" % ws)
+    if world != gpus:
+        raise SystemExit("bench.py: WORLD_SIZE=%d but --gpus %d; launch one rank per GPU "
+                         "(torch.distributed.run --nproc-per-node %d ... bench.py --gpus %d)"
+                         % (world, gpus, gpus, gpus))
+    return ("run", world)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_command(n, argv, port):
+    """torch.distributed.run over this script with the same arguments: one
+    rank per GPU of this node, rendezvous on 127.0.0.1."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % n,
+            "--master-addr=127.0.0.1", "--master-port=%d" % port, os.path.abspath(__file__)] + list(argv)
+
+
+def spawn_ranks(n, argv):
+    """Start the N rank processes as a child (nothing in this process has
+    touched the GPU) and return its exit status; rank 0's JSON line reaches
+    stdout through the inherited descriptor."""
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on these hosts
+    cmd = spawn_command(n, argv, _free_port())
+    print("[bench] launching %d ranks: %s" % (n, " ".join(cmd)), file=sys.stderr, flush=True)
+    return subprocess.call(cmd, env=env)
+
+
+def agree_all(flag, world, backend, dev):
+    """True on every rank iff `flag` is true on every rank (MIN over the
+    process group), so that all ranks take the same branch before a
+    collective-carrying HIP graph is replayed."""
+    if world <= 1:
+        return bool(flag)
+    t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=dev if backend == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item())
+
+
+def timed_region(step, steps, warmup, world, every, stream, S, graph_mode, backend, dev):
+    """W untimed warmup steps, then K timed steps bracketed by a barrier and a
+    device sync on both sides; returns (elapsed max over ranks, profiled
+    steps, whether a HIP graph was replayed).  Per-kernel hipEvents on every
+    `every`-th step (or on as many extra steps after a graph replay)."""
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    graph = None
+    if graph_mode:
+        ok = True
+        try:
+            graph = S.Graph(step, stream)
+            graph.launch()  # one untimed replay
+            torch.cuda.synchronize()
+        except S.SrcnnError as e:  # e.g. a collective that cannot be captured
+            print("[bench] HIP graph capture failed (%s)" % e, file=sys.stderr)
+            ok = False
+        # every rank must take the same branch: a graph replay carries the
+        # all-reduce, so mixed graph / direct ranks would mismatch collectives
+        if not agree_all(ok, world, backend, dev):
+            if graph is not None:
+                graph.close()
+            graph = None
+            print("[bench] HIP graph not used on every rank; timing direct calls", file=sys.stderr)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    S.profile_reset()
+    n_prof = 0
+    t0 = time.perf_counter()
+    if graph is not None:
+        for _ in range(steps):
+            graph.launch()
+    else:
+        for i in range(steps):
+            on = i % every == every - 1
+            n_prof += on
+            S.profile_enable(on)
+            step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    S.profile_enable(False)
+    if graph is not None:
+        n_prof = max(1, steps // every)
+        S.profile_enable(True)
+        for _ in range(n_prof):
+            step()
+        torch.cuda.synchronize()
+        S.profile_enable(False)
+        graph.close()
+    if world > 1:
+        e = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    return elapsed, n_prof, graph is not None
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs of this node, one rank each; without torch.distributed.run the "
+                         "ranks are launched by this script")
     # defaults: the kernels reach their steady clock after ~25 steps of a
     # fresh process (rocprofv3 trace: d1 485 -> 432 us over the first 25
     # launches, flat over the next 275), so the default run warms up past it
@@ -528,21 +667,25 @@ def main():
     # default; torch.distributed then only ships the RCCL id and runs the
     # barriers / max-time reduction (gloo).  --comm torch uses dist.all_reduce.
     ap.add_argument("--comm", choices=["srcnn", "torch"], default="srcnn")
-    # the timed steps replay one HIP graph of the step (srcnn_graph_*): the
-    # same kernels and collective without a host launch per kernel.  Default:
-    # on for N > 1 with --global-batch (strong scaling: small per-rank steps,
-    # where host launch jitter between the ranks' collectives shows), off
-    # otherwise: at N = 1 it measured the same (0.8975 vs 0.894 ms, same box),
-    # and at 4096 tiles per rank the launches hide under the kernels, so the
-    # weak-scaling line keeps the direct calls (a captured multi-rank RCCL
-    # collective has only been replayed on a one-rank communicator here)
+    # --graph on: the timed steps replay one HIP graph of the step
+    # (srcnn_graph_*): the same kernels and collective without a host launch
+    # per kernel; the ranks agree on its use (agree_all) before any replay.
+    # Default off: at N = 1 it measured the same (0.8975 vs 0.894 ms, same
+    # box), the direct calls enqueue well ahead of the GPU even at 512 tiles
+    # per rank, and a captured multi-rank RCCL collective has not been
+    # replayed on more than one GPU yet
     ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto")
+    ap.add_argument("--no-strong", action="store_true",
+                    help="N > 1: skip the strong-scaling sub-record (global batch 4096)")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default=None,
                     help="process-group backend (default: gloo with --comm srcnn, nccl with torch)")
     # rehearsal of the N>1 path on a single-GPU box (NOT a measurement):
     # every rank on one device, gradients all-reduced over gloo
     ap.add_argument("--all-ranks-on-device", type=int, default=None)
     args = ap.parse_args()
+    mode, world = launch_plan(args.gpus, os.environ)
+    if mode == "spawn":
+        sys.exit(spawn_ranks(world, sys.argv[1:]))
 
     import srcnn_amd as S
     from srcnn_amd import parallel
@@ -572,28 +715,44 @@ def main():
         global_tiles = B * world
     w, h = TILE, TILE
     P = S.net_param_count(net)
+    # the strong-scaling sub-record (N > 1) reuses the first tiles of this
+    # rank's batch, so allocate for the larger of the two shards
+    Bs = parallel.shard(STRONG_GLOBAL_BATCH, rank, world)[1] if world > 1 else 0
+    Bmax = max(B, Bs, 1)
     rng = np.random.default_rng(1234 + rank)
-    X, T = synthetic_batch(rng, max(B, 1), w, h)
+    X, T = synthetic_batch(rng, Bmax, w, h)
     prm = init_params(net_t, P)
     Xd = torch.from_numpy(X).to(dev)
     Td = torch.from_numpy(T).to(dev)
     params = torch.from_numpy(prm).to(dev)
     grads = torch.zeros(P, dtype=torch.float32, device=dev)
     mom = torch.zeros(P, dtype=torch.float32, device=dev)
-    ws_bytes = S.train_workspace_bytes(net, w, h, max(B, 1))
+    ws_bytes = S.train_workspace_bytes(net, w, h, Bmax)
     ws = torch.empty(ws_bytes // 4 + 64, dtype=torch.float32, device=dev)
     lr = [1e-4, 1e-4, 1e-5]
 
     comm = None
+    rccl_ranks = None
     if world > 1 and args.comm == "srcnn":
         comm = parallel.SrcnnComm(S, stream)
-    # one rank's shard of the global batch -> grads; one all-reduce; the same
-    # update on every rank (srcnn_amd/parallel.py)
-    step = parallel.DataParallelStep(
-        grads,
-        lambda g: S.train_fwd_bwd(net, Xd, Td, w, h, B, params, g, None, ws, ws_bytes, stream),
-        lambda nb: S.update_all(net, params, grads, mom, 0.9, 1e-3, lr, nb, stream),
-        global_tiles, allreduce=comm)
+        # what the communicator itself reports, not what the launcher asked for
+        c_rank, rccl_ranks = S.comm_rank(comm.comm)
+        if rccl_ranks != world or c_rank != rank:
+            raise SystemExit("bench.py: RCCL communicator has rank %d of %d, expected %d of %d"
+                             % (c_rank, rccl_ranks, rank, world))
+    elif world > 1 and backend == "nccl":
+        rccl_ranks = dist.get_world_size()
+
+    def dp_step(batch, global_batch):
+        """One rank's shard -> grads; one all-reduce; the same update on every
+        rank (srcnn_amd/parallel.py)."""
+        return parallel.DataParallelStep(
+            grads,
+            lambda g: S.train_fwd_bwd(net, Xd, Td, w, h, batch, params, g, None, ws, ws_bytes, stream),
+            lambda nb: S.update_all(net, params, grads, mom, 0.9, 1e-3, lr, nb, stream),
+            global_batch, allreduce=comm)
+
+    step = dp_step(B, global_tiles)
     if world == 1 and not os.environ.get("SRCNN_BENCH_SEPARATE_UPDATE"):
         # one device, no exchange: srcnn_train_step (the same step; on the
         # fused path the update runs inside the gradient reduction).
@@ -628,68 +787,38 @@ def main():
     torch.cuda.synchronize()
     _mark("side legs done")
 
-    for i in range(args.warmup):
-        step()
-        if i == 0:
-            _mark("first warmup step enqueued")
-    torch.cuda.synchronize()
-    _mark("warmup done")
-    use_graph = (args.graph == "on" or (args.graph == "auto" and world > 1 and strong)) and \
-        (world == 1 or comm is not None)
-    graph = None
-    if use_graph:
-        try:
-            graph = S.Graph(step, stream)
-            graph.launch()  # one untimed replay
-            torch.cuda.synchronize()
-        except S.SrcnnError as e:  # e.g. a collective that cannot be captured: time the calls
-            print("[bench] HIP graph capture failed (%s); timing direct calls" % e, file=sys.stderr)
-            graph = None
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    S.profile_reset()
-    # Per-kernel durations come from hipEvent pairs recorded around the
-    # launches of every `profile_every`-th step of the timed region (steps
-    # every-1, 2*every-1, ...: the first step after the warmup sync starts
-    # cold).  Event pairs around every launch cost 2.5% of the step even as
-    # fence-free timing events (1.011 vs 0.986 ms, same box), so the sampled
-    # steps carry the instrumentation and the others run bare.
-    # With the graph, every timed step is a bare replay and the per-kernel
-    # durations come from as many profiled (non-graph) steps right after the
-    # timed region, at the same steady clock.
+    graph_mode = args.graph == "on" and (world == 1 or comm is not None)
     every = max(1, min(args.profile_every, args.steps))
-    n_prof = 0
-    t0 = time.perf_counter()
-    if graph is not None:
-        for i in range(args.steps):
-            graph.launch()
-    else:
-        for i in range(args.steps):
-            on = i % every == every - 1
-            n_prof += on
-            S.profile_enable(on)
-            step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    S.profile_enable(False)
-    elapsed = t1 - t0
-    if graph is not None:
-        n_prof = max(1, args.steps // every)
-        S.profile_enable(True)
-        for i in range(n_prof):
-            step()
-        torch.cuda.synchronize()
-        S.profile_enable(False)
-        graph.close()
+    # Per-kernel durations come from hipEvent pairs recorded around the
+    # launches of every `every`-th timed step (steps every-1, 2*every-1, ...:
+    # the first step after the warmup sync starts cold).  Event pairs around
+    # every launch cost 2.5% of the step even as fence-free timing events
+    # (1.011 vs 0.986 ms, same box), so the sampled steps carry the
+    # instrumentation and the others run bare.
+    elapsed, n_prof, used_graph = timed_region(step, args.steps, args.warmup, world, every, stream, S,
+                                               graph_mode, backend, dev)
+    _mark("headline timed steps done")
     kernel_path = S.last_path()
-    if world > 1:
-        e = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
-        dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        elapsed = float(e.item())
     stats = S.profile_stats()
+
+    # N > 1: the strong-scaling step in the same run (global batch 4096
+    # sharded over the ranks: 512 tiles per rank at N = 8), timed the same way
+    strong_rec = None
+    if world > 1 and not strong and not args.no_strong:
+        sstep = dp_step(Bs, STRONG_GLOBAL_BATCH)
+        s_el, s_prof, s_graph = timed_region(sstep, args.steps, args.warmup, world, every, stream, S,
+                                             graph_mode, backend, dev)
+        s_stats = S.profile_stats()
+        s_ms = s_el / args.steps * 1e3
+        strong_rec = {
+            "scaling": "strong", "global_batch": STRONG_GLOBAL_BATCH, "batch_per_gpu": Bs,
+            "value": round(STRONG_GLOBAL_BATCH * args.steps / s_el, 1), "unit": "tiles/s",
+            "ms_per_step": round(s_ms, 4), "steps": args.steps, "warmup": args.warmup,
+            "hip_graph": s_graph,
+            "kernels": {k: {"launches_per_step": c / max(s_prof, 1), "ms_per_step": round(t / max(s_prof, 1), 4)}
+                        for k, (c, t) in s_stats.items()},
+            "note": "rank 0's per-kernel split; value = 4096 tiles x steps / max-over-ranks time"}
+        _mark("strong timed steps done")
     assert np.isfinite(params.cpu().numpy()).all(), "non-finite parameters after training"
     fwd_sharded = None
     if world > 1 and not args.no_forward:
@@ -728,6 +857,11 @@ def main():
             workload = ("SRCNN default n1=64 n2=32 f1=9 f2=1 f3=5, fp32 training, 33x33 luma tiles, "
                         "batch %d per GPU (BASELINE.json configs[1]%s)"
                         % (B, ", configs[2] weak scaling" if world > 1 else ""))
+        if world == 1 and not strong and B == STRONG_GLOBAL_BATCH:
+            # at N = 1 the strong-scaling step IS the headline step
+            strong_rec = {"scaling": "strong", "global_batch": B, "batch_per_gpu": B,
+                          "value": round(value, 1), "unit": "tiles/s", "ms_per_step": round(ms_step, 4),
+                          "note": "N = 1: the headline step (global batch 4096 on one GPU)"}
         out = {
             "metric": metric,
             "value": round(value, 1),
@@ -744,13 +878,16 @@ def main():
             "config": {"workload": workload, "global_batch": global_tiles, "batch_per_gpu": B,
                        "tile": "33x33", "parallelism": "dp%d" % world,
                        "kernel_path": kernel_path,
-                       "hip_graph": graph is not None,
+                       "hip_graph": used_graph,
                        "step_call": ("srcnn_train_fwd_bwd + srcnn_update_all" if world > 1 or
                                      os.environ.get("SRCNN_BENCH_SEPARATE_UPDATE") else
                                      "srcnn_train_step (SGD update inside the gradient reduction)"),
                        "grad_allreduce": (("srcnn_allreduce_grads (RCCL)" if comm else
                                            "torch.distributed all_reduce (%s)" % backend)
-                                          if world > 1 else None)},
+                                          if world > 1 else None),
+                       "rccl_ranks": rccl_ranks,
+                       "launcher": ("torch.distributed.run" if os.environ.get("TORCHELASTIC_RUN_ID")
+                                    else "env") if world > 1 else None},
             "roofline": roof,
             "rooflines": rooflines,
             "step_roofline": step_roofline(step_roof_ms(stats, n_prof, work, B), t_roof * 1e3, ms_step),
@@ -758,6 +895,8 @@ def main():
             "profiled_steps": n_prof,
             "cpu_baseline": None,
         }
+        if strong_rec is not None:
+            out["strong"] = strong_rec
         if fwd_sharded is not None:
             out["forward"] = fwd_sharded
         out.update(side)

@@ -1580,7 +1580,10 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   if (lds3 > 64 * 1024) return 0;
   // wl3l: A2 image + Q + delta3 grid (the reduction reuses the A2 image)
   const size_t lds3l = (size_t)(npx2 * N2 + npx2 * F3 * F3 + (g.w3 + 2 * (F3 - 1)) * (g.h3 + 2 * (F3 - 1))) * 4;
-  const bool wl3l = kWl3Lds && lds3l <= 160 * 1024 && npx2 * N2 >= 2 * 16 * 64 * 8 && g.w3 * g.h3 <= 512;
+  // the 160 KiB LDS also holds wl3l's static red_s[2][8] (64 B)
+  constexpr size_t kWl3lStaticLds = 2 * 8 * sizeof(float);
+  const bool wl3l = kWl3Lds && lds3l + kWl3lStaticLds <= 160 * 1024 && npx2 * N2 >= 2 * 16 * 64 * 8 &&
+                    g.w3 * g.h3 <= 512;
   constexpr int NPD = N1 / 64;  // delta1 items per sample (64-channel parts)
   const int GD = std::min(g.batch * NPD, 256);  // a multiple of NPD: block parity = part
   const int G1 = GD / NPD;                      // gW1 slabs: one per block pair

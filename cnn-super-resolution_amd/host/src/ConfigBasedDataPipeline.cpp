@@ -309,6 +309,22 @@ void ConfigBasedDataPipeline::update_parameters(LayerAllocationPool& l1, LayerAl
                            _config->weight_decay_parameter, lr, uint32_t(batch), _context->stream()),
           "update_parameters");
   } else {
+    // caller-owned pools: momentum read from the parameters file
+    // (set_save_momentum checkpoints) goes into their previous_batch_delta_*
+    // buffers before the first update, as bind_flat does for the flat ones
+    const LayerData* layers[3] = {&layer_data_1, &layer_data_2, &layer_data_3};
+    for (int i = 0; i < 3; ++i)
+      for (int k = 0; k < 2; ++k) {
+        auto& v = _momentum_in[i][k];
+        if (v.empty()) continue;
+        const size_t n = k ? layers[i]->bias_size() : layers[i]->weight_size();
+        srcnn::require(v.size() == n, "parameters file: layer " + std::to_string(i + 1) + " momentum has " +
+                                          std::to_string(v.size()) + " values, expected " + std::to_string(n));
+        MemoryHandle& m = k ? pools[i]->previous_batch_delta_b : pools[i]->previous_batch_delta_w;
+        if (m == gpu_nullptr) m = _context->allocate(srcnn::MEM_READ_WRITE, n * sizeof(float));
+        _context->write_buffer(m, 0, n * sizeof(float), v.data(), true);  // size-checked
+        v.clear();
+      }
     DataPipeline::update_parameters(layer_data_3, l3, batch, _config->momentum,
                                     _config->weight_decay_parameter, _config->learning_rate[2], ev);
     DataPipeline::update_parameters(layer_data_2, l2, batch, _config->momentum,

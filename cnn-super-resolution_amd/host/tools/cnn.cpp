@@ -311,21 +311,35 @@ class HostSumExchange {
  private:
   void barrier() {
     std::unique_lock<std::mutex> lk(_mu);
+    if (_aborted) throw std::runtime_error("host exchange: another rank failed");
     const unsigned gen = _gen;
     if (++_arrived == _n) {
       _arrived = 0;
       ++_gen;
       _cv.notify_all();
     } else {
-      _cv.wait(lk, [&] { return _gen != gen; });
+      _cv.wait(lk, [&] { return _gen != gen || _aborted; });
+      if (_gen == gen) throw std::runtime_error("host exchange: another rank failed");
     }
   }
+
+ public:
+  /** A failing rank releases the ranks parked in barrier(): they throw
+   * instead of waiting for an arrival that will never come. */
+  void abort() {
+    std::lock_guard<std::mutex> lk(_mu);
+    _aborted = true;
+    _cv.notify_all();
+  }
+
+ private:
   const int _n;
   std::vector<std::vector<float>> _slots;
   std::mutex _mu;
   std::condition_variable _cv;
   int _arrived = 0;
   unsigned _gen = 0;
+  bool _aborted = false;
 };
 
 /** `train --devices N`: one thread per device, each with its own Context
@@ -360,10 +374,18 @@ int train_data_parallel(const Config& cfg, const Args& a) {
         pipeline.init(DataPipeline::LOAD_KERNEL_ALL);
         rcs[r] = train(pipeline, a, seed, ex[r].get(), r, n);
       } catch (const std::exception& e) {
-        // the other ranks may be parked in a collective this one will never
-        // join: report and leave without unwinding them
         std::cout << "[ERROR] rank " << r << ": " << e.what() << std::endl;
         std::cout.flush();
+        if (a.host_exchange) {
+          // the host-sum seam: release the ranks parked in its barrier (they
+          // throw and report in turn), then join them as usual
+          host.abort();
+          rcs[r] = 1;
+          return;
+        }
+        // RCCL: the other ranks may be parked in a collective this one will
+        // never join and cannot be released from here; leave without
+        // unwinding them
         _exit(1);
       }
     });
