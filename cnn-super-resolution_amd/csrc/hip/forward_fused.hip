@@ -20,6 +20,9 @@
 // frame are computed on zero-padded inputs; they only reach outputs past the
 // frame, which are never stored.  Each (tap row dy, partial row) pair of the
 // LDS accumulator is written by exactly one chunk, so no atomics are needed.
+#include <cstdlib>
+#include <cstring>
+
 #include "common.hpp"
 #include "mfma.hpp"
 #include "ops.hpp"
@@ -71,7 +74,12 @@ struct FwdGeom {
   int batch;
 };
 
-template <int N1, int N2, int F1, int F3>
+// QT: Q held transposed per wave, [tap][pixel slot] at a row stride of 52
+// floats (= 20 mod 32), so the window sums' LDS reads of consecutive items
+// fall in consecutive banks (the [pixel][tap] image at stride 36 put 4 items
+// on one bank: 4-way conflicts); the Q stores become 16 ds_write_b32 per
+// lane instead of 4 ds_write_b128
+template <int N1, int N2, int F1, int F3, bool QT>
 __global__ __launch_bounds__(256, SRCNN_FWD_WAVES) void fwd_l123_kernel(
     const float* __restrict__ X, const float* __restrict__ W1, const float* __restrict__ B1,
     const float* __restrict__ W2, const float* __restrict__ B2, const float* __restrict__ W3,
@@ -85,18 +93,28 @@ __global__ __launch_bounds__(256, SRCNN_FWD_WAVES) void fwd_l123_kernel(
   static_assert(K3 <= 32 && N2 <= 32 && N2 % 2 == 0 && K1 % 2 == 1, "Q tile shape");
   __shared__ float xs[kFwdXs];
   // per-wave Q[pixel + F3-1][tap]: F3-1 zero rows either side, so a window
-  // sum reads its F3 taps without bounds tests
+  // sum reads its F3 taps without bounds tests (QT: Q^T[tap][pixel + F3-1],
+  // F3-1 zero columns either side)
   constexpr int QR = kFwdRW + 2 * (F3 - 1);
-  __shared__ __attribute__((aligned(16))) float qs[4][QR][QS];
+  constexpr int QTS = 52;  // QT row stride: 5 x 52 = 4 (mod 32), item (dy, e) -> bank 36 dy + e (mod 32)
+  static_assert(QR <= QTS, "Q^T row");
+  __shared__ __attribute__((aligned(16))) float qs[4][QT ? 32 : QR][QT ? QTS : QS];
   __shared__ float accs[F3][EHM][EW];  // [dy][partial row][partial col]
 
   SRCNN_CLOCK_BEGIN();
   const int lane = mfma::lane_id(), wave = mfma::wave_id();
   const int h = lane >> 5, li = lane & 31;
   const int EH = g.rh + F3 - 1;
-  for (int i = threadIdx.x; i < 4 * 2 * (F3 - 1) * QS; i += 256) {  // the zero rows (never written again)
-    const int w = i / (2 * (F3 - 1) * QS), r = (i / QS) % (2 * (F3 - 1)), col = i % QS;
-    qs[w][r < F3 - 1 ? r : kFwdRW + r][col] = 0.0f;
+  if constexpr (QT) {
+    for (int i = threadIdx.x; i < 4 * 32 * 2 * (F3 - 1); i += 256) {  // the zero columns (never written again)
+      const int w = i / (64 * (F3 - 1)), r = (i / (2 * (F3 - 1))) % 32, col = i % (2 * (F3 - 1));
+      qs[w][r][col < F3 - 1 ? col : kFwdRW + col] = 0.0f;
+    }
+  } else {
+    for (int i = threadIdx.x; i < 4 * 2 * (F3 - 1) * QS; i += 256) {  // the zero rows (never written again)
+      const int w = i / (2 * (F3 - 1) * QS), r = (i / QS) % (2 * (F3 - 1)), col = i % QS;
+      qs[w][r < F3 - 1 ? r : kFwdRW + r][col] = 0.0f;
+    }
   }
   // L3 window sums: this lane's items k of the F3 x EW (tap row dy, column e)
   // per chunk, as a base into the wave's Q image (taps dx follow at a stride
@@ -106,7 +124,7 @@ __global__ __launch_bounds__(256, SRCNN_FWD_WAVES) void fwd_l123_kernel(
 #pragma unroll
   for (int k = 0; k < kWin; k++) {
     const int it = min(lane + 64 * k, F3 * EW - 1), dy = it / EW, e = it - dy * EW;
-    wrb[k] = (wave * QR + e) * QS + dy * F3;
+    wrb[k] = QT ? (wave * 32 + dy * F3) * QTS + e : (wave * QR + e) * QS + dy * F3;
     wwb[k] = (dy * EHM + F3 - 1 - dy) * EW + e;
   }
 
@@ -223,11 +241,17 @@ __global__ __launch_bounds__(256, SRCNN_FWD_WAVES) void fwd_l123_kernel(
       f32x16 accq = zero16();
 #pragma unroll
       for (int s = 0; s < 16; s++) accq = mma(w3f[s], acc2[s], accq);
-      // Q[pixel li][taps crow(r, h)]: 4 runs of 4 consecutive taps per lane
+      if constexpr (QT) {
+        // Q^T[taps crow(r, h)][pixel li]: 16 rows per lane, lanes consecutive
 #pragma unroll
-      for (int q = 0; q < 4; q++)
-        *reinterpret_cast<float4*>(&qs[wave][li + F3 - 1][8 * q + 4 * h]) =
-            make_float4(accq[4 * q], accq[4 * q + 1], accq[4 * q + 2], accq[4 * q + 3]);
+        for (int r = 0; r < 16; r++) qs[wave][crow(r, h)][li + F3 - 1] = accq[r];
+      } else {
+        // Q[pixel li][taps crow(r, h)]: 4 runs of 4 consecutive taps per lane
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+          *reinterpret_cast<float4*>(&qs[wave][li + F3 - 1][8 * q + 4 * h]) =
+              make_float4(accq[4 * q], accq[4 * q + 1], accq[4 * q + 2], accq[4 * q + 3]);
+      }
       __builtin_amdgcn_wave_barrier();
       // tap row dy of this chunk feeds partial row c + F3 - 1 - dy:
       //   accs[dy][c + F3-1 - dy][e] = sum_dx Q[e - (F3-1) + dx][dy*F3 + dx]
@@ -243,7 +267,7 @@ __global__ __launch_bounds__(256, SRCNN_FWD_WAVES) void fwd_l123_kernel(
           const float* qr = &qs[0][0][0] + wrb[k];
           float v = 0.0f;
 #pragma unroll
-          for (int dx = 0; dx < F3; dx++) v += qr[dx * (QS + 1)];
+          for (int dx = 0; dx < F3; dx++) v += qr[dx * ((QT ? QTS : QS) + 1)];
           (&accs[0][0][0])[wwb[k] + c * EW] = v;
         }
       }
@@ -304,6 +328,12 @@ __global__ __launch_bounds__(256) void fwd_seam_kernel(const float* __restrict__
   }
 }
 
+// SRCNN_FWD_Q=rows: the [pixel][tap] Q image (A/B; read per call)
+static bool fwd_qt() {
+  const char* e = std::getenv("SRCNN_FWD_Q");
+  return !(e && std::strcmp(e, "rows") == 0);
+}
+
 template <int N1, int N2, int F1, int F3>
 int run_forward(const float* X, uint32_t w, uint32_t h, uint32_t batch, const float* params,
                 float* out, void* ws, size_t ws_bytes, hipStream_t s, bool query_only,
@@ -333,8 +363,12 @@ int run_forward(const float* X, uint32_t w, uint32_t h, uint32_t batch, const fl
   const float* B3 = W3 + F3 * F3 * N2;
   {
     SRCNN_PROFILE("fwd_l123_mfma", s);
-    hipLaunchKernelGGL((fwd_l123_kernel<N1, N2, F1, F3>), dim3((unsigned)std::min<long>(items, SRCNN_FWD_GRID)),
-                       dim3(256), 0, s, X, W1, B1, W2, B2, W3, part, g);
+    if (fwd_qt())
+      hipLaunchKernelGGL((fwd_l123_kernel<N1, N2, F1, F3, true>), dim3((unsigned)std::min<long>(items, SRCNN_FWD_GRID)),
+                         dim3(256), 0, s, X, W1, B1, W2, B2, W3, part, g);
+    else
+      hipLaunchKernelGGL((fwd_l123_kernel<N1, N2, F1, F3, false>), dim3((unsigned)std::min<long>(items, SRCNN_FWD_GRID)),
+                         dim3(256), 0, s, X, W1, B1, W2, B2, W3, part, g);
     SRCNN_LAUNCH_TRY();
   }
   {
@@ -366,8 +400,9 @@ int preload_forward(const srcnn_net* net) {
   if (net->f2 != 1) return 0;
 #define SRCNN_FWD_CASE(A, B, C, D)                                                        \
   if (net->n1 == A && net->n2 == B && net->f1 == C && net->f3 == D) {                    \
-    const void* k[] = {(const void*)fwd_l123_kernel<A, B, C, D>, (const void*)fwd_seam_kernel<D>}; \
-    int rc = resolve_kernels(k, 2);                                                      \
+    const void* k[] = {(const void*)fwd_l123_kernel<A, B, C, D, true>,                   \
+                       (const void*)fwd_l123_kernel<A, B, C, D, false>, (const void*)fwd_seam_kernel<D>}; \
+    int rc = resolve_kernels(k, 3);                                                      \
     return rc ? rc : 1;                                                                  \
   }
   SRCNN_FWD_CASE(64, 32, 9, 5)

@@ -218,15 +218,6 @@ __global__ void prepack_w2_kernel(const float* __restrict__ W2, float* __restric
 // the DMA instructions go out as one burst in the chunk's first tap, after
 // that tap's B loads, so only the B waits of tap 4 cover them.
 // ---------------------------------------------------------------------------
-// the next chunk's LDS-DMA in kDmaSplit bursts, at taps 0, kDmaEvery, ...
-#ifndef SRCNN_WIDE_DMA_SPLIT
-#define SRCNN_WIDE_DMA_SPLIT 1
-#endif
-#ifndef SRCNN_WIDE_DMA_EVERY
-#define SRCNN_WIDE_DMA_EVERY 8
-#endif
-constexpr int kDmaSplit = SRCNN_WIDE_DMA_SPLIT, kDmaEvery = SRCNN_WIDE_DMA_EVERY;
-static_assert(kDmaSplit >= 1 && (kDmaSplit - 1) * kDmaEvery < 25, "DMA bursts within the chunk's taps");
 constexpr int kImgMax = 960;                  // pixels of one chunk image (<= 31 x 31)
 constexpr int kImgSlack = 256;                // floats: one DMA instruction past the image
 
@@ -277,126 +268,29 @@ inline int conv_windows(const CGeom& g) {
   return g.wo == 0 ? 1 : ((g.out_w + g.wo - 1) / g.wo) * ((g.out_h + g.wo - 1) / g.wo);
 }
 
-constexpr int kXBuf = kXTile + 64;  // X tile buffer of the fused gW1 epilogue
+constexpr int kXBuf = kXTile + 64;  // X tile buffer of the fused gW1 epilogue (d1g16)
 
-// F1 > 0 (delta1 only): gW1 / gB1 fused into the epilogue.  The masked delta1
-// tile in the accumulators is directly the B operand of gW1 += Xwin^T delta1
-// (register s of half h is pixel crow(s, h), mfma.hpp), so delta1 never
-// leaves the CU; A = X windows (81 taps + a ones row for gB1, 3 x 32 rows)
-// from a per-item X tile DMA'd into LDS.  One gW1 slab per pair of blocks
-// (block parity = the 64-channel part, fixed because the grid is even).
-// diagnostics builds only (results invalid), delta1 + gW1 variant: 1 drop the
-// gW1 MFMAs, 2 drop the relu' mask loads, 4 drop the next-chunk LDS-DMA
-#ifdef SRCNN_WIDE_DIAG
-constexpr int kWDiag = SRCNN_WIDE_DIAG;
-#else
-constexpr int kWDiag = 0;
-#endif
-template <int CIN, int COUT, int F, int MT, bool DELTA, int F1>
+template <int CIN, int COUT, int F, int MT, bool DELTA>
 __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restrict__ in,
                                                           const float* __restrict__ Wimg,
                                                           const float* __restrict__ bias,
                                                           const float* __restrict__ ycur,
-                                                          float* __restrict__ out,
-                                                          const float* __restrict__ X,
-                                                          float* __restrict__ slab1, CGeom g) {
+                                                          float* __restrict__ out, CGeom g) {
   constexpr int NCH = CIN / kCC, FF = F * F, KSC = FF * (kCC / 8), KS = NCH * KSC;
   constexpr int NP = COUT / 64;
-  constexpr bool G1 = DELTA && F1 > 0;
-  constexpr int NT1 = F1 * F1, TT = G1 ? (NT1 + 1 + 31) / 32 : 1;
   static_assert(CIN % kCC == 0 && COUT % 64 == 0 && kCC == 16, "shape");
   extern __shared__ float smem[];
   const int lane = lane_id(), wave = wave_id(), j = lane & 31, h = lane >> 5;
   const int nt = wave & 1, mg = wave >> 1;
   const int buf_floats = g.img_w * g.img_h * kPS + kImgSlack;  // the largest window image
   const int nitems = g.batch * NP * (g.wo == 0 ? 1 : ((g.out_w + g.wo - 1) / g.wo) * ((g.out_h + g.wo - 1) / g.wo));
-  float* const xsm = smem + 2 * buf_floats;  // G1: 2 X tile buffers (item parity)
-  int toffx[TT];
-  float fill[TT];
-  bool valid[TT];
-  f32x16 gacc[TT];
-#pragma unroll
-  for (int tt = 0; tt < TT; tt++) {
-    const int tap = 32 * tt + j, tc = min(tap, NT1 - 1);
-    valid[tt] = tap < NT1;
-    fill[tt] = tap == NT1 ? 1.0f : 0.0f;
-    toffx[tt] = G1 ? (tc / F1) * kXS + tc % F1 : 0;
-    gacc[tt] = zero16();
-  }
-  // X tile of item it -> xsm[parity] by 4-byte LDS-DMA (stride kXS, zero fill;
-  // G1 runs single-window only, so the item's image is it / NP)
-  auto xdma = [&](int it, int par) {
-    const int s = it / NP;
-    float* dst = xsm + par * kXBuf;
-    for (int k = wave; k * 64 < kXTile; k += 4) {
-      const int f = k * 64 + lane, row = f / kXS, col = f - row * kXS;
-      const bool ok = row < g.xh && col < g.xw;
-      dma4(ok ? X + (size_t)s * g.xw * g.xh + row * g.xw + col : g_zero_src, dst + k * 64);
-    }
-  };
   int abase[MT];
   // delta1: a tap row dy whose image rows are zero border for every pixel of
   // tile m (dy outside [dlo, dhi]) is skipped for that tile (wave-uniform
   // branches around MFMA groups that hold no memory operations)
   int dlo[MT], dhi[MT];
-  // G1 (delta1 of whole 33x33-class tiles): the M tiles hold the output
-  // pixels in a class-grouped order instead of raster order.  A pixel's class
-  // is (row class, column class): the 4 border rows / columns at each edge
-  // are classes of their own, the interior one class; its valid taps (those
-  // whose delta2 source is inside the image, not the zero border) are the
-  // same for every pixel of a class.  Tiles filled class by class (row class
-  // order interior, top, bottom; column classes left to right; each class
-  // column by column) issue the taps that no pixel of the tile can use far
-  // less often: at 25x25 outputs 12,768 instead of 13,760 pixel-taps for
-  // 11,025 useful ones (-7.2% MFMAs).  ptab[slot] = pixel of M-tile slot
-  // (the 32 * (2m + mg) + j of raster order; slots past the image repeat
-  // its last pixel, masked in the epilogue like before), ptab[kSlots + tile]
-  // = the tile's 25-bit mask of taps any of its pixels can use.
-  constexpr int kSlots = 2 * MT * 32;
-  int* const ptab = reinterpret_cast<int*>(xsm + 2 * kXBuf);
-  uint32_t tmask[MT];
-  if constexpr (G1) {
-    const int ow = g.out_w, oh = g.out_h, B = F - 1;
-    if (threadIdx.x == 0) {
-      int n = 0;
-      if (ow < 2 * B + 1 || oh < 2 * B + 1 || ow * oh > kSlots) {
-        for (; n < ow * oh && n < kSlots; n++) ptab[n] = n;  // raster order
-      } else {
-        // class c of an extent e: c < B the single row / column c, c == B the
-        // interior [B, e - B), c > B the single row / column e - 2B - 1 + c
-        auto lo = [&](int c, int e) { return c < B ? c : (c == B ? B : e - 2 * B - 1 + c); };
-        auto hi = [&](int c, int e) { return c < B ? c + 1 : (c == B ? e - B : e - 2 * B + c); };
-        for (int yo = 0; yo <= 2 * B; yo++) {
-          const int yc = yo == 0 ? B : (yo <= B ? yo - 1 : yo);
-          for (int xc = 0; xc <= 2 * B; xc++)
-            for (int x = lo(xc, ow); x < hi(xc, ow); x++)
-              for (int y = lo(yc, oh); y < hi(yc, oh); y++) ptab[n++] = y * ow + x;
-        }
-      }
-      for (; n < kSlots; n++) ptab[n] = ow * oh - 1;
-    }
-    __syncthreads();
-    // tile masks: slot i's taps, OR-reduced over the tile's 32 slots (half a wave)
-    for (int i = threadIdx.x; i < kSlots; i += 256) {
-      const int pix = ptab[i], y = pix / ow, x = pix - y * ow;
-      uint32_t mbits = 0;
-#pragma unroll
-      for (int dy = 0; dy < F; dy++)
-#pragma unroll
-        for (int dx = 0; dx < F; dx++) {
-          const bool ok = y + dy >= g.pad && y + dy < g.pad + g.in_h && x + dx >= g.pad && x + dx < g.pad + g.in_w;
-          mbits |= ok ? 1u << (dy * F + dx) : 0u;
-        }
-#pragma unroll
-      for (int o = 1; o < 32; o <<= 1) mbits |= __shfl_xor(mbits, o, 64);
-      if ((i & 31) == 0) ptab[kSlots + i / 32] = (int)mbits;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int m = 0; m < MT; m++) tmask[m] = __builtin_amdgcn_readfirstlane(ptab[kSlots + 2 * m + mg]);
-  }
-  // the image pixel of M-tile slot `slot` (raster order unless G1)
-  auto pix_of = [&](int slot, int npxw_) { return G1 ? ptab[slot] : min(slot, npxw_ - 1); };
+  // the image pixel of M-tile slot `slot` (raster order)
+  auto pix_of = [&](int slot, int npxw_) { return min(slot, npxw_ - 1); };
   // one LDS-DMA instruction k (64 slots of 16 B) of chunk c of window wn
   // (every window's image is img_w wide: pix / img_w as a multiply, exact for
   // pix < 4096; the predicate is formed without short-circuit branches)
@@ -421,8 +315,8 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restri
   }
   wait_vm0();
   __syncthreads();
-  int bsel = 0, ipar = 0;
-  for (int it = blockIdx.x; it < nitems; it += gridDim.x, ipar ^= 1) {
+  int bsel = 0;
+  for (int it = blockIdx.x; it < nitems; it += gridDim.x) {
     const CWin cw = conv_win<F, NP>(it, g);
     const int s = cw.s, part = cw.part, npxw = cw.ow * cw.oh;
     // the next item's window (its first chunk is staged under this item's last)
@@ -435,7 +329,6 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restri
       dlo[m] = __builtin_amdgcn_readfirstlane(g.pad - (cw.y0 + pb / cw.ow));
       dhi[m] = __builtin_amdgcn_readfirstlane(g.pad + g.in_h - 1 - (cw.y0 + pa / cw.ow));
     }
-    if constexpr (G1) xdma(it, ipar);  // lands before the first chunk barrier
     const float4* wp = reinterpret_cast<const float4*>(Wimg) + (size_t)(part * 2 + nt) * KS * 64 + lane;
     f32x16 acc[MT];
 #pragma unroll
@@ -483,11 +376,8 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restri
           // taps (2 per tap), the DMAs were waited on 3 taps after issue; as
           // one burst at tap 0 only the B loads of tap 4 wait for them
           // (same-box A/B: delta1 + gW1 -1.0%, L2 forward -1.0%)
-          if (stage && !(kWDiag & 4) && t % kDmaEvery == 0 && t / kDmaEvery < kDmaSplit) {
-            const int part_ = t / kDmaEvery, lo = kdma * part_ / kDmaSplit, hi = kdma * (part_ + 1) / kDmaSplit;
-            for (int k = wave; k < kdma; k += 4)
-              if (k >= lo && k < hi) dma(wd, nc, nxt, k);
-          }
+          if (stage && t == 0)
+            for (int k = wave; k < kdma; k += 4) dma(wd, nc, nxt, k);
           // k-step (t, 0) while (t, 1) loads; k-step (t, 1) while (t + 1, 0)
           // loads.  sched_barriers pin the order: left alone, the scheduler
           // sinks the prefetch reads below the MFMAs and exposes LDS latency.
@@ -497,7 +387,7 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restri
           __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
           for (int m = 0; m < MT; m++)
-            if (!DELTA || (G1 ? ((tmask[m] >> t) & 1u) != 0 : (dy >= dlo[m] && dy <= dhi[m]))) {
+            if (!DELTA || (dy >= dlo[m] && dy <= dhi[m])) {
 #pragma unroll
               for (int jj = 0; jj < 4; jj++) acc[m] = mma(a[m][jj], bq[dx][0][jj], acc[m]);
             }
@@ -508,7 +398,7 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restri
           __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
           for (int m = 0; m < MT; m++)
-            if (!DELTA || (G1 ? ((tmask[m] >> t) & 1u) != 0 : (dy >= dlo[m] && dy <= dhi[m]))) {
+            if (!DELTA || (dy >= dlo[m] && dy <= dhi[m])) {
 #pragma unroll
               for (int jj = 0; jj < 4; jj++) acc[m] = mma(an[m][jj], bq[dx][1][jj], acc[m]);
             }
@@ -520,66 +410,9 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restri
       bsel ^= 1;
     }
     const int n = part * 64 + nt * 32 + j;
-    // output pixels of the window, from its origin (G1: one window per image)
+    // output pixels of the window, from its origin
     const size_t obase = ((size_t)s * g.npx + (size_t)cw.y0 * g.out_w + cw.x0) * COUT + n;
-    if constexpr (G1) {
-      // delta1 = relu'(A1) * acc (mask loads one tile ahead), then
-      // gW1 += Xwin^T delta1 on the matrix core
-      const float* xs = xsm + ipar * kXBuf;
-      float mk[16], mkn[16];
-#pragma unroll
-      for (int r = 0; r < 16; r++) {
-        const int pix = pix_of(32 * mg + crow(r, h), g.npx);
-        mk[r] = (kWDiag & 2) ? 1.0f : ycur[obase + (size_t)pix * COUT];
-      }
-#pragma unroll
-      for (int m = 0; m < MT; m++) {
-        int hl = h;
-        asm volatile("" : "+v"(hl));
-        const int p0 = 32 * (2 * m + mg) + 4 * hl;
-        if (m + 1 < MT) {
-#pragma unroll
-          for (int r = 0; r < 16; r++) {
-            const int pix = pix_of(p0 + 64 + crow(r, 0), g.npx);
-            mkn[r] = (kWDiag & 2) ? 1.0f : ycur[obase + (size_t)pix * COUT];
-          }
-        }
-#pragma unroll
-        for (int r = 0; r < 16; r++) {
-          const int pix = p0 + crow(r, 0);
-          acc[m][r] = (pix < g.npx && mk[r] > 0.0f) ? acc[m][r] : 0.0f;
-        }
-        // X windows of k-step r (pixel crow(r, h) of the tile) read two k-steps
-        // ahead into a ring of three named register sets, pinned by
-        // sched_barriers: left alone, the scheduler reads each window right
-        // before its MFMA and this one wave per SIMD waits out the LDS latency
-        float xq[3][TT];
-        auto xrd = [&](int r) {
-          const int pix = pix_of(p0 + crow(r, 0), g.npx), py = pix / g.out_w;
-          const int xb = py * kXS + pix - py * g.out_w;
-#pragma unroll
-          for (int tt = 0; tt < TT; tt++) xq[r % 3][tt] = xs[xb + toffx[tt]];
-        };
-        xrd(0);
-        xrd(1);
-#pragma unroll
-        for (int r = 0; r < 16; r++) {
-          if (r + 2 < 16) xrd(r + 2);
-          __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-          for (int tt = 0; tt < TT; tt++) {
-            const float av = xq[r % 3][tt];
-            if (!(kWDiag & 1)) gacc[tt] = mma(valid[tt] ? av : fill[tt], acc[m][r], gacc[tt]);
-            else gacc[tt][0] += acc[m][r] + av;
-          }
-          __builtin_amdgcn_sched_barrier(0);
-        }
-        if (m + 1 < MT) {
-#pragma unroll
-          for (int r = 0; r < 16; r++) mk[r] = mkn[r];
-        }
-      }
-    } else {
+    {
       const float bn = DELTA ? 0.0f : bias[n];
       const uint32_t ow_mag = (1u << 20) / (uint32_t)cw.ow + 1u;  // exact for pix < 4096
       // one 32-pixel tile at a time; the lane index is made opaque per tile so
@@ -606,37 +439,11 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restri
       }
     }
   }
-  if constexpr (G1) {
-    // gW1 slab of this block pair: waves mg = 1 park their partials in LDS,
-    // waves mg = 0 add them (fixed order) and store rows tap < NT1 (+ gB1 row)
-    constexpr int P1 = NT1 * COUT + COUT;
-    __syncthreads();
-    float* red = smem;
-    if (mg == 1) {
-#pragma unroll
-      for (int tt = 0; tt < TT; tt++)
-#pragma unroll
-        for (int r = 0; r < 16; r++) red[((nt * TT + tt) * 16 + r) * 64 + lane] = gacc[tt][r];
-    }
-    __syncthreads();
-    if (mg == 0) {
-      const int ch = (blockIdx.x % NP) * 64 + 32 * nt + j;
-      float* o1 = slab1 + (size_t)(blockIdx.x / NP) * P1;
-#pragma unroll
-      for (int tt = 0; tt < TT; tt++)
-#pragma unroll
-        for (int r = 0; r < 16; r++) {
-          const int tap = 32 * tt + crow(r, h);
-          const float v = gacc[tt][r] + red[((nt * TT + tt) * 16 + r) * 64 + lane];
-          if (tap <= NT1) o1[tap * COUT + ch] = v;
-        }
-    }
-  }
 }
 
 // ---------------------------------------------------------------------------
 // d1g16: delta1 + gW1 of the wide training step on 16-pixel M tiles (round 3).
-// The same contraction as conv_mfma<DELTA, F1> (delta1 = relu'(A1) * (delta2
+// The same contraction as conv_mfma<DELTA> (delta1 = relu'(A1) * (delta2
 // padded by F-1 (*) W2 flipped / transposed), then gW1 += Xwin^T delta1 and
 // gB1 from a ones row), on v_mfma_f32_16x16x4_f32 instead of 32x32x2: the
 // same FLOPs per cycle and the same operand reads per MAC, but the border
@@ -655,10 +462,6 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restri
 //   channel n, i.e. directly gW1's B operand (K = the 4 pixel slots); A = the
 //   X windows of 16-tap tiles (81 taps + the ones row: 6 tiles)
 // ---------------------------------------------------------------------------
-#ifndef SRCNN_WIDE_D16
-#define SRCNN_WIDE_D16 1
-#endif
-constexpr bool kWideD16 = SRCNN_WIDE_D16;
 #ifndef SRCNN_D16_MASK_AHEAD
 #define SRCNN_D16_MASK_AHEAD 3  // epilogue relu' loads run this many tiles ahead
 #endif
@@ -825,11 +628,8 @@ __global__ __launch_bounds__(256, 1) void d1g16_kernel(const float* __restrict__
 #pragma unroll
           for (int q = 0; q < 2; q++) bq[(dx + F - 1) % F][q] = wp[(size_t)q * WQ + kb * 64];
           // the next chunk's whole DMA in the first tap, after its B loads (conv_mfma)
-          if (stage && !(kWDiag & 4) && t % kDmaEvery == 0 && t / kDmaEvery < kDmaSplit) {
-            const int part_ = t / kDmaEvery, lo = kdma * part_ / kDmaSplit, hi = kdma * (part_ + 1) / kDmaSplit;
-            for (int k = wave; k < kdma; k += 4)
-              if (k >= lo && k < hi) dma(nit / NP, nc, nxt, k);
-          }
+          if (stage && t == 0)
+            for (int k = wave; k < kdma; k += 4) dma(nit / NP, nc, nxt, k);
           // tiles MH.. of tap t load while tiles ..MH of tap t run
 #pragma unroll
           for (int m = 0; m < MH; m++) an[m] = *reinterpret_cast<const float4*>(cur + abase[MH + m] + toff);
@@ -1182,10 +982,6 @@ __global__ __launch_bounds__(256, 2) void wl3_kernel(const float* __restrict__ A
 // waves per CU; the next sample's first Q tile is loaded before the delta2
 // stores (a store counts in vmcnt too) and lands under delta2 / gW3.
 // ---------------------------------------------------------------------------
-#ifndef SRCNN_WL3_LDS
-#define SRCNN_WL3_LDS 1
-#endif
-constexpr bool kWl3Lds = SRCNN_WL3_LDS;
 template <int N2>
 __device__ __forceinline__ int wl3l_at(int p, int c) {  // A2 image float index, quads XOR-swizzled by pixel
   return p * N2 + 4 * ((c >> 2) ^ (p & (N2 / 4 - 1))) + (c & 3);
@@ -1386,13 +1182,6 @@ struct G2Geom {
                      // tap offsets stay scalar: 4 adds per k-step, not 7)
 };
 
-// diagnostics builds only (results invalid): 1 drop the MFMAs, 2 drop the
-// staging DMA after the first band, 4 drop the band barrier
-#ifdef SRCNN_WG2_DIAG
-constexpr int kWg2Diag = SRCNN_WG2_DIAG;
-#else
-constexpr int kWg2Diag = 0;
-#endif
 template <int CIN, int COUT, int F>
 __global__ __launch_bounds__(512, 1) void wgrad2_kernel(const float* __restrict__ A1,
                                                        const float* __restrict__ D2,
@@ -1466,9 +1255,9 @@ __global__ __launch_bounds__(512, 1) void wgrad2_kernel(const float* __restrict_
   if (nunits > 0) stage(0, smem);
   for (int u = 0; u < nunits; u++) {
     wait_vm0();
-    if (!(kWg2Diag & 4) || u == 0) __syncthreads();  // unit u landed; everyone is done with the other buffer
+    __syncthreads();  // unit u landed; everyone is done with the other buffer
     const float* cur = smem + (bsel ? kGBuf : 0);
-    if (u + 1 < nunits && !(kWg2Diag & 2)) stage(u + 1, smem + (bsel ? 0 : kGBuf));
+    if (u + 1 < nunits) stage(u + 1, smem + (bsel ? 0 : kGBuf));
     // k-step kq's operands (delta2 value + the F*F A1 taps) are read one
     // k-step ahead into two named register sets, pinned by sched_barriers:
     // left alone, the scheduler reads two taps at a time right before their
@@ -1489,8 +1278,7 @@ __global__ __launch_bounds__(512, 1) void wgrad2_kernel(const float* __restrict_
 #pragma unroll
       for (int t = 0; t < FF; t++) {
         const float a = av[kq & 1][t];
-        if (kWg2Diag & 1) acc[t][0] += a * b;
-        else acc[t] = mma16(a, b, acc[t]);
+        acc[t] = mma16(a, b, acc[t]);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -1582,7 +1370,7 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   const size_t lds3l = (size_t)(npx2 * N2 + npx2 * F3 * F3 + (g.w3 + 2 * (F3 - 1)) * (g.h3 + 2 * (F3 - 1))) * 4;
   // the 160 KiB LDS also holds wl3l's static red_s[2][8] (64 B)
   constexpr size_t kWl3lStaticLds = 2 * 8 * sizeof(float);
-  const bool wl3l = kWl3Lds && lds3l + kWl3lStaticLds <= 160 * 1024 && npx2 * N2 >= 2 * 16 * 64 * 8 &&
+  const bool wl3l = lds3l + kWl3lStaticLds <= 160 * 1024 && npx2 * N2 >= 2 * 16 * 64 * 8 &&
                     g.w3 * g.h3 <= 512;
   constexpr int NPD = N1 / 64;  // delta1 items per sample (64-channel parts)
   const int GD = std::min(g.batch * NPD, 256);  // a multiple of NPD: block parity = part
@@ -1616,7 +1404,7 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   {
     SRCNN_PROFILE("wide_prepack_w2", s);
     const int tot = 2 * NetT::W2;
-    hipLaunchKernelGGL((prepack_w2_kernel<N1, N2, F2, kWideD16>), dim3((tot + 255) / 256), dim3(256), 0, s,
+    hipLaunchKernelGGL((prepack_w2_kernel<N1, N2, F2, true>), dim3((tot + 255) / 256), dim3(256), 0, s,
                        W2, Wf, Wd);
     SRCNN_LAUNCH_TRY();
   }
@@ -1629,11 +1417,10 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   {
     SRCNN_PROFILE("wide_l2_fwd", s);
     const size_t lds = 2 * ((size_t)cf.img_w * cf.img_h * kPS + kImgSlack) * sizeof(float);
-    if (int rc = set_lds(conv_mfma_kernel<N1, N2, F2, NetT::MT2, false, 0>, lds)) return rc;
+    if (int rc = set_lds(conv_mfma_kernel<N1, N2, F2, NetT::MT2, false>, lds)) return rc;
     const int items = g.batch * (N2 / 64);
-    hipLaunchKernelGGL((conv_mfma_kernel<N1, N2, F2, NetT::MT2, false, 0>), dim3(std::min(items, GC)),
-                       dim3(256), lds, s, A1, Wf, B2, (const float*)nullptr, A2, (const float*)nullptr,
-                       (float*)nullptr, cf);
+    hipLaunchKernelGGL((conv_mfma_kernel<N1, N2, F2, NetT::MT2, false>), dim3(std::min(items, GC)),
+                       dim3(256), lds, s, A1, Wf, B2, (const float*)nullptr, A2, cf);
     SRCNN_LAUNCH_TRY();
   }
   {
@@ -1651,18 +1438,10 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   }
   {
     SRCNN_PROFILE("wide_delta1_grad1", s);
-    if (kWideD16) {
-      const size_t lds = (2 * ((size_t)cd.img_w * cd.img_h * kPS + kImgSlack) + 2 * kXBuf + kD16Slots +
-                          4 * kD16MT) * sizeof(float);  // + the slot -> pixel table, tile masks, tile order
-      if (int rc = set_lds(d1g16_kernel<N2, N1, F2, F1>, lds)) return rc;
-      hipLaunchKernelGGL((d1g16_kernel<N2, N1, F2, F1>), dim3(GD), dim3(256), lds, s, D2, Wd, A1, X, slab1, cd);
-    } else {
-      const size_t lds = (2 * ((size_t)cd.img_w * cd.img_h * kPS + kImgSlack) + 2 * kXBuf +
-                          2 * NetT::MT4 * 33) * sizeof(float);  // + the class-order pixel table
-      if (int rc = set_lds(conv_mfma_kernel<N2, N1, F2, NetT::MT4, true, F1>, lds)) return rc;
-      hipLaunchKernelGGL((conv_mfma_kernel<N2, N1, F2, NetT::MT4, true, F1>), dim3(GD), dim3(256),
-                         lds, s, D2, Wd, (const float*)nullptr, A1, (float*)nullptr, X, slab1, cd);
-    }
+    const size_t lds = (2 * ((size_t)cd.img_w * cd.img_h * kPS + kImgSlack) + 2 * kXBuf + kD16Slots +
+                        4 * kD16MT) * sizeof(float);  // + the slot -> pixel table, tile masks, tile order
+    if (int rc = set_lds(d1g16_kernel<N2, N1, F2, F1>, lds)) return rc;
+    hipLaunchKernelGGL((d1g16_kernel<N2, N1, F2, F1>), dim3(GD), dim3(256), lds, s, D2, Wd, A1, X, slab1, cd);
     SRCNN_LAUNCH_TRY();
   }
   {
@@ -1779,13 +1558,13 @@ int op_conv_fwd(const float* in, float* out, const float* W, const float* B, uin
   if (w2i.rc()) return w2i.rc();
   float* img = w2i.img();
   const size_t lds = 2 * ((size_t)cf.img_w * cf.img_h * kPS + kImgSlack) * sizeof(float);
-  if (int rc = set_lds(conv_mfma_kernel<kWN1, kWN2, kWF, WideNet::MT2, false, 0>, lds)) return rc;
+  if (int rc = set_lds(conv_mfma_kernel<kWN1, kWN2, kWF, WideNet::MT2, false>, lds)) return rc;
   {
     SRCNN_PROFILE("conv_fwd_wide_mfma", s);
     const int items = (int)batch * (kWN2 / 64) * conv_windows(cf);
-    hipLaunchKernelGGL((conv_mfma_kernel<kWN1, kWN2, kWF, WideNet::MT2, false, 0>),
+    hipLaunchKernelGGL((conv_mfma_kernel<kWN1, kWN2, kWF, WideNet::MT2, false>),
                        dim3(std::min(items, 256)), dim3(256), lds, s, in, img, B,
-                       (const float*)nullptr, out, (const float*)nullptr, (float*)nullptr, cf);
+                       (const float*)nullptr, out, cf);
     SRCNN_LAUNCH_TRY();
   }
   return 1;
@@ -1809,14 +1588,13 @@ int op_conv_delta(const float* d_next, const float* y_curr, float* d_curr, const
   if (w2i.rc()) return w2i.rc();
   float* img = w2i.img();
   const size_t lds = 2 * ((size_t)cd.img_w * cd.img_h * kPS + kImgSlack) * sizeof(float);
-  if (int rc = set_lds(conv_mfma_kernel<kWN2, kWN1, kWF, WideNet::MT4, true, 0>, lds)) return rc;
+  if (int rc = set_lds(conv_mfma_kernel<kWN2, kWN1, kWF, WideNet::MT4, true>, lds)) return rc;
   {
     SRCNN_PROFILE("conv_delta_wide_mfma", s);
     const int items = (int)batch * (kWN1 / 64) * conv_windows(cd);
-    hipLaunchKernelGGL((conv_mfma_kernel<kWN2, kWN1, kWF, WideNet::MT4, true, 0>),
+    hipLaunchKernelGGL((conv_mfma_kernel<kWN2, kWN1, kWF, WideNet::MT4, true>),
                        dim3(std::min(items, 256)), dim3(256), lds, s, d_next,
-                       img + align_f(WideNet::W2), (const float*)nullptr, y_curr, d_curr,
-                       (const float*)nullptr, (float*)nullptr, cd);
+                       img + align_f(WideNet::W2), (const float*)nullptr, y_curr, d_curr, cd);
     SRCNN_LAUNCH_TRY();
   }
   return 1;
@@ -1882,12 +1660,14 @@ int op_conv_grad_acc(const float* in, const float* d, float* gW, float* gB, uint
 int preload(const srcnn_net* net) {
   if (!(net->n1 == 128 && net->n2 == 64 && net->f1 == 9 && net->f2 == 5 && net->f3 == 5)) return 0;
   using NetT = WideNet;
-  const void* k[] = {(const void*)prepack_w2_kernel<128, 64, 5>, (const void*)wl1_fwd_kernel<128, 9>,
-                     (const void*)conv_mfma_kernel<128, 64, 5, NetT::MT2, false, 0>,
-                     (const void*)wl3_kernel<64, 5>,
-                     (const void*)conv_mfma_kernel<64, 128, 5, NetT::MT4, true, 9>,
-                     (const void*)wgrad2_kernel<128, 64, 5>};
-  int rc = resolve_kernels(k, 6);
+  // the training step's kernels (and the op-level delta1 / forward ones)
+  const void* k[] = {(const void*)prepack_w2_kernel<128, 64, 5, true>, (const void*)wl1_fwd_kernel<128, 9>,
+                     (const void*)conv_mfma_kernel<128, 64, 5, NetT::MT2, false>,
+                     (const void*)wl3l_kernel<64, 5>, (const void*)wl3_kernel<64, 5>,
+                     (const void*)d1g16_kernel<64, 128, 5, 9>,
+                     (const void*)conv_mfma_kernel<64, 128, 5, NetT::MT4, true>,
+                     (const void*)prepack_w2_kernel<128, 64, 5>, (const void*)wgrad2_kernel<128, 64, 5>};
+  int rc = resolve_kernels(k, 9);
   return rc ? rc : 1;
 }
 

@@ -520,6 +520,48 @@ def test_train_step_nonsquare_tiles(S, w, h, batch):
         assert_close(got[sl], rg[sl], RTOL, "grad " + nm, xg[sl], FLIP_FLOOR)
 
 
+@pytest.mark.parametrize("l3", ["stream", "tile"])
+@pytest.mark.parametrize("batch,w,h", [(16, 33, 33), (512, 33, 33), (769, 33, 33), (7, 35, 31), (3, 39, 39),
+                                       (2, 21, 21)])
+def test_train_step_l3_kernels_vs_oracle(S, monkeypatch, l3, batch, w, h):
+    """Layer 3 of the fused step on both kernels: the whole-tile
+    l3_delta_kernel (SRCNN_L3=tile, the default) and the unit-stream
+    l3s_kernel (SRCNN_L3=stream: 768 resident blocks, a ragged last round at
+    769 tiles), gradients, squared error and A3 against the oracle
+    (last_layer_delta.cl, layer_deltas.cl, backpropagate.cl)."""
+    monkeypatch.setenv("SRCNN_L3", l3)
+    cfg = NETS["default"]
+    net = S.Net(*cfg)
+    rng = np.random.default_rng(31)
+    X, T = make_batch(rng, batch, w, h)
+    params = make_params(rng, cfg, sd=0.05)
+    P = params.size
+    g0 = (1e-3 * rng.standard_normal(P)).astype(np.float32)
+    rg, _ = orc.train_fwd_bwd(cfg, X, T, w, h, batch, params, g0)
+    xg, _ = orc.f64.train_fwd_bwd(cfg, X, T, w, h, batch, params, g0)
+    nbytes = S.train_workspace_bytes(net, w, h, batch)
+    ws = torch.empty(nbytes // 4 + 64, dtype=torch.float32, device="cuda")
+    g, err = D(g0), zeros(1)
+    S.train_fwd_bwd(net, D(X), D(T), w, h, batch, D(params), g, err, ws, nbytes)
+    assert S.last_path() == "fused", S.last_path()
+    got = H(g)
+    off = S.net_offsets(net) + [P]
+    for i, nm in enumerate(["W1", "B1", "W2", "B2", "W3", "B3"]):
+        sl = slice(off[i], off[i + 1])
+        assert_close(got[sl], rg[sl], RTOL, "l3 %s grad %s" % (l3, nm), xg[sl], FLIP_FLOOR)
+    pad = cfg[2] + cfg[3] + cfg[4] - 3
+    A3 = orc.forward(cfg, X, w, h, batch, params)
+    ref_err = orc.sq_err(T, A3, w, h, w - pad, h - pad, batch)
+    assert float(H(err)[0]) == pytest.approx(ref_err, rel=1e-4)
+    # A3 as left in the workspace (srcnn_train_activations)
+    n1, n2 = cfg[0], cfg[1]
+    w1, h1 = w - cfg[2] + 1, h - cfg[2] + 1
+    w3, h3 = w1 - cfg[4] + 1, h1 - cfg[4] + 1
+    A1d, A2d, A3d = zeros(batch * w1 * h1 * n1), zeros(batch * w1 * h1 * n2), zeros(batch * w3 * h3)
+    S.train_activations(net, w, h, batch, ws, nbytes, A1d, A2d, A3d)
+    assert_close(H(A3d), A3, RTOL, "l3 %s A3" % l3)
+
+
 def test_forward_vs_oracle(S, path):
     cfg = NETS["default"]
     net = S.Net(*cfg)
