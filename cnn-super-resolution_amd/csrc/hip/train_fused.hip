@@ -952,6 +952,8 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   // ranges (work items), so the grid still fills every CU's 4 block slots
   const int nch1 = (ow * oh + 31) / 32;
   int d1c_parts = kD1c ? std::max(1, std::min({4, nch1, kD1cGrid / (int)std::max<uint32_t>(batch, 1)})) : 1;
+  if (const char* e = std::getenv("SRCNN_D1C_PARTS"))  // A/B of the small-batch split (read per call)
+    if (kD1c && std::atoi(e) > 0) d1c_parts = std::min({4, nch1, std::atoi(e)});
   while (d1c_parts > 1 && (d1c_parts - 1) * ((nch1 + d1c_parts - 1) / d1c_parts) >= nch1)
     d1c_parts--;  // every part holds at least one chunk (the kernel's DMA pipeline assumes it)
   const int gd = kD1c ? (int)std::min<size_t>((size_t)batch * d1c_parts, kD1cGrid) : grid_for_batch(batch, 512);

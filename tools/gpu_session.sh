@@ -10,8 +10,13 @@ export TMPDIR=/tmp
 ok() { local rc=$1; [ "$rc" -eq 0 ] || [ "$rc" -eq 1 ]; }
 
 echo "== rocm-smi" && (rocm-smi --showproductname > "$OUT/smi.txt" 2>&1 || true)
-timeout -k 10 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider > "$OUT/pytest_gpu.log" 2>&1
+# every parity check logs its achieved errors (tests/hip_util.py); the raw log
+# and its summary go under profiles/ with the session
+rm -f "$OUT/parity_checks.jsonl"
+SRCNN_PARITY_LOG=$PWD/$OUT/parity_checks.jsonl timeout -k 10 900 python -u -m pytest tests -m gpu -q -x \
+  --timeout 300 --timeout-method thread -p no:cacheprovider > "$OUT/pytest_gpu.log" 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -5 "$OUT/pytest_gpu.log"
+[ -s "$OUT/parity_checks.jsonl" ] && python3 tools/parity_summary.py "$OUT/parity_checks.jsonl" > "$OUT/parity_summary.json"
 ok $rc || exit $rc
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
 rc=$?; echo "smoke rc=$rc"; tail -3 "$OUT/smoke.log"

@@ -34,6 +34,8 @@ def main(path):
         "rounding_clause_checks": len(bounded),
         "rounding_clause_elements_past_rtol": sum(r["n_over_rtol"] for r in bounded),
         "rounding_ratio_max": max((r["rounding_ratio_max"] for r in bounded), default=None),
+        "rounding_clause_scale": "0.25 x the probabilistic estimate u sqrt(n) sum|terms| (hip_util.K_ROUND)",
+        "rounding_only_elements": sum(r.get("n_round_only", 0) for r in bounded),
         "flip_records": len(flips),
         "flips_total": {k: sum(r[k] for r in flips) for k in ("flips_A1", "flips_A2", "flips_A3")},
         "ambiguous_total": {k: sum(r[k] for r in flips) for k in ("ambiguous_A1", "ambiguous_A2", "ambiguous_A3")},
