@@ -20,9 +20,6 @@
 // frame are computed on zero-padded inputs; they only reach outputs past the
 // frame, which are never stored.  Each (tap row dy, partial row) pair of the
 // LDS accumulator is written by exactly one chunk, so no atomics are needed.
-#include <cstdlib>
-#include <cstring>
-
 #include "common.hpp"
 #include "mfma.hpp"
 #include "ops.hpp"
@@ -74,12 +71,7 @@ struct FwdGeom {
   int batch;
 };
 
-// QT: Q held transposed per wave, [tap][pixel slot] at a row stride of 52
-// floats (= 20 mod 32), so the window sums' LDS reads of consecutive items
-// fall in consecutive banks (the [pixel][tap] image at stride 36 put 4 items
-// on one bank: 4-way conflicts); the Q stores become 16 ds_write_b32 per
-// lane instead of 4 ds_write_b128
-template <int N1, int N2, int F1, int F3, bool QT>
+template <int N1, int N2, int F1, int F3>
 __global__ __launch_bounds__(256, SRCNN_FWD_WAVES) void fwd_l123_kernel(
     const float* __restrict__ X, const float* __restrict__ W1, const float* __restrict__ B1,
     const float* __restrict__ W2, const float* __restrict__ B2, const float* __restrict__ W3,
@@ -87,34 +79,29 @@ __global__ __launch_bounds__(256, SRCNN_FWD_WAVES) void fwd_l123_kernel(
   constexpr int K1 = F1 * F1, KS1 = (K1 + 1) / 2, NT1 = N1 / 32;
   constexpr int K3 = F3 * F3;
   constexpr int TW = kFwdRW + F1 - 1;  // LDS row stride of the input tile
-  constexpr int QS = 36;               // Q row: 32 taps + pad, 16-B aligned
   constexpr int EW = kFwdRW + F3 - 1;  // partial-sum window width
   constexpr int EHM = kFwdRhMax + F3 - 1;
   static_assert(K3 <= 32 && N2 <= 32 && N2 % 2 == 0 && K1 % 2 == 1, "Q tile shape");
   __shared__ float xs[kFwdXs];
-  // per-wave Q[pixel + F3-1][tap]: F3-1 zero rows either side, so a window
-  // sum reads its F3 taps without bounds tests (QT: Q^T[tap][pixel + F3-1],
-  // F3-1 zero columns either side)
+  // per-wave Q^T[tap][pixel + F3-1]: F3-1 zero columns either side, so a
+  // window sum reads its F3 taps without bounds tests.  Row stride 52 floats
+  // (5 x 52 = 4 mod 32): the window-sum items (dy, e) of one ds_read_b32 fall
+  // in consecutive banks.  (Round 3 held Q as [pixel][tap] at stride 36 with
+  // float4 stores; its window-sum reads were 4-way bank conflicted: same-box
+  // A/B, 4 pairs, the frame 0.4-1.0% faster this way, profiles/r04_ab_fwdq.)
   constexpr int QR = kFwdRW + 2 * (F3 - 1);
-  constexpr int QTS = 52;  // QT row stride: 5 x 52 = 4 (mod 32), item (dy, e) -> bank 36 dy + e (mod 32)
+  constexpr int QTS = 52;
   static_assert(QR <= QTS, "Q^T row");
-  __shared__ __attribute__((aligned(16))) float qs[4][QT ? 32 : QR][QT ? QTS : QS];
+  __shared__ __attribute__((aligned(16))) float qs[4][32][QTS];
   __shared__ float accs[F3][EHM][EW];  // [dy][partial row][partial col]
 
   SRCNN_CLOCK_BEGIN();
   const int lane = mfma::lane_id(), wave = mfma::wave_id();
   const int h = lane >> 5, li = lane & 31;
   const int EH = g.rh + F3 - 1;
-  if constexpr (QT) {
-    for (int i = threadIdx.x; i < 4 * 32 * 2 * (F3 - 1); i += 256) {  // the zero columns (never written again)
-      const int w = i / (64 * (F3 - 1)), r = (i / (2 * (F3 - 1))) % 32, col = i % (2 * (F3 - 1));
-      qs[w][r][col < F3 - 1 ? col : kFwdRW + col] = 0.0f;
-    }
-  } else {
-    for (int i = threadIdx.x; i < 4 * 2 * (F3 - 1) * QS; i += 256) {  // the zero rows (never written again)
-      const int w = i / (2 * (F3 - 1) * QS), r = (i / QS) % (2 * (F3 - 1)), col = i % QS;
-      qs[w][r < F3 - 1 ? r : kFwdRW + r][col] = 0.0f;
-    }
+  for (int i = threadIdx.x; i < 4 * 32 * 2 * (F3 - 1); i += 256) {  // the zero columns (never written again)
+    const int w = i / (64 * (F3 - 1)), r = (i / (2 * (F3 - 1))) % 32, col = i % (2 * (F3 - 1));
+    qs[w][r][col < F3 - 1 ? col : kFwdRW + col] = 0.0f;
   }
   // L3 window sums: this lane's items k of the F3 x EW (tap row dy, column e)
   // per chunk, as a base into the wave's Q image (taps dx follow at a stride
@@ -124,7 +111,7 @@ __global__ __launch_bounds__(256, SRCNN_FWD_WAVES) void fwd_l123_kernel(
 #pragma unroll
   for (int k = 0; k < kWin; k++) {
     const int it = min(lane + 64 * k, F3 * EW - 1), dy = it / EW, e = it - dy * EW;
-    wrb[k] = QT ? (wave * 32 + dy * F3) * QTS + e : (wave * QR + e) * QS + dy * F3;
+    wrb[k] = (wave * 32 + dy * F3) * QTS + e;
     wwb[k] = (dy * EHM + F3 - 1 - dy) * EW + e;
   }
 
@@ -241,17 +228,9 @@ __global__ __launch_bounds__(256, SRCNN_FWD_WAVES) void fwd_l123_kernel(
       f32x16 accq = zero16();
 #pragma unroll
       for (int s = 0; s < 16; s++) accq = mma(w3f[s], acc2[s], accq);
-      if constexpr (QT) {
-        // Q^T[taps crow(r, h)][pixel li]: 16 rows per lane, lanes consecutive
+      // Q^T[taps crow(r, h)][pixel li]: 16 rows per lane, lanes consecutive
 #pragma unroll
-        for (int r = 0; r < 16; r++) qs[wave][crow(r, h)][li + F3 - 1] = accq[r];
-      } else {
-        // Q[pixel li][taps crow(r, h)]: 4 runs of 4 consecutive taps per lane
-#pragma unroll
-        for (int q = 0; q < 4; q++)
-          *reinterpret_cast<float4*>(&qs[wave][li + F3 - 1][8 * q + 4 * h]) =
-              make_float4(accq[4 * q], accq[4 * q + 1], accq[4 * q + 2], accq[4 * q + 3]);
-      }
+      for (int r = 0; r < 16; r++) qs[wave][crow(r, h)][li + F3 - 1] = accq[r];
       __builtin_amdgcn_wave_barrier();
       // tap row dy of this chunk feeds partial row c + F3 - 1 - dy:
       //   accs[dy][c + F3-1 - dy][e] = sum_dx Q[e - (F3-1) + dx][dy*F3 + dx]
@@ -267,7 +246,7 @@ __global__ __launch_bounds__(256, SRCNN_FWD_WAVES) void fwd_l123_kernel(
           const float* qr = &qs[0][0][0] + wrb[k];
           float v = 0.0f;
 #pragma unroll
-          for (int dx = 0; dx < F3; dx++) v += qr[dx * ((QT ? QTS : QS) + 1)];
+          for (int dx = 0; dx < F3; dx++) v += qr[dx * (QTS + 1)];
           (&accs[0][0][0])[wwb[k] + c * EW] = v;
         }
       }
@@ -328,12 +307,6 @@ __global__ __launch_bounds__(256) void fwd_seam_kernel(const float* __restrict__
   }
 }
 
-// SRCNN_FWD_Q=rows: the [pixel][tap] Q image (A/B; read per call)
-static bool fwd_qt() {
-  const char* e = std::getenv("SRCNN_FWD_Q");
-  return !(e && std::strcmp(e, "rows") == 0);
-}
-
 template <int N1, int N2, int F1, int F3>
 int run_forward(const float* X, uint32_t w, uint32_t h, uint32_t batch, const float* params,
                 float* out, void* ws, size_t ws_bytes, hipStream_t s, bool query_only,
@@ -363,12 +336,8 @@ int run_forward(const float* X, uint32_t w, uint32_t h, uint32_t batch, const fl
   const float* B3 = W3 + F3 * F3 * N2;
   {
     SRCNN_PROFILE("fwd_l123_mfma", s);
-    if (fwd_qt())
-      hipLaunchKernelGGL((fwd_l123_kernel<N1, N2, F1, F3, true>), dim3((unsigned)std::min<long>(items, SRCNN_FWD_GRID)),
-                         dim3(256), 0, s, X, W1, B1, W2, B2, W3, part, g);
-    else
-      hipLaunchKernelGGL((fwd_l123_kernel<N1, N2, F1, F3, false>), dim3((unsigned)std::min<long>(items, SRCNN_FWD_GRID)),
-                         dim3(256), 0, s, X, W1, B1, W2, B2, W3, part, g);
+    hipLaunchKernelGGL((fwd_l123_kernel<N1, N2, F1, F3>), dim3((unsigned)std::min<long>(items, SRCNN_FWD_GRID)),
+                       dim3(256), 0, s, X, W1, B1, W2, B2, W3, part, g);
     SRCNN_LAUNCH_TRY();
   }
   {
@@ -400,9 +369,8 @@ int preload_forward(const srcnn_net* net) {
   if (net->f2 != 1) return 0;
 #define SRCNN_FWD_CASE(A, B, C, D)                                                        \
   if (net->n1 == A && net->n2 == B && net->f1 == C && net->f3 == D) {                    \
-    const void* k[] = {(const void*)fwd_l123_kernel<A, B, C, D, true>,                   \
-                       (const void*)fwd_l123_kernel<A, B, C, D, false>, (const void*)fwd_seam_kernel<D>}; \
-    int rc = resolve_kernels(k, 3);                                                      \
+    const void* k[] = {(const void*)fwd_l123_kernel<A, B, C, D>, (const void*)fwd_seam_kernel<D>}; \
+    int rc = resolve_kernels(k, 2);                                                      \
     return rc ? rc : 1;                                                                  \
   }
   SRCNN_FWD_CASE(64, 32, 9, 5)

@@ -791,7 +791,6 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
 #define SRCNN_D1C 1  // n1 = 64, n2 = 32: kernel 3 in the cooperative-chunk form (d1c.hpp)
 #endif
 #include "d1c.hpp"
-#include "l3_stream.hpp"
 
 // ---------------------------------------------------------------------------
 // deterministic slab reduction: dst[i] += sum_b slab[b][i] in a fixed order
@@ -899,14 +898,6 @@ struct Net {
 
 static int grid_for_batch(uint32_t batch, int cap) { return (int)std::min<uint32_t>(batch, cap); }
 
-// layer 3 of the default net: the whole-tile l3_delta_kernel, or with
-// SRCNN_L3=stream the unit-stream l3s_kernel (l3_stream.hpp; A/B and its
-// tests, read per call)
-static bool l3s_enabled() {
-  const char* e = std::getenv("SRCNN_L3");
-  return e && std::strcmp(e, "stream") == 0;
-}
-
 template <int N2, int F3>
 static int launch_l3(const float* A2, const float* T, const float* W3, const float* B3, float* D2,
                      float* slab3, float* sqs, float* A3, const L3Geom& lg, int grid, size_t lds,
@@ -940,20 +931,16 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   // keep l12 and d1 and run layer 3 through the op-level kernels instead
   // (ops_fast.hip: L3 forward, last delta, delta2, gW3 over HWC A2 / A3 / D3).
   const size_t lds3 = l3_lds_bytes<N2, F3>(ow, oh);
-  const int l3s_L1 = (N2 == 32 && F3 == 5 && l3s_enabled()) ? l3s_lag(ow, oh, F3) : 0;
   const bool l3_fused =
-      l3s_L1 > 0 ||
-      (lds3 <= 160 * 1024 && w3 * h3 <= kL3MaxOut &&
-       ((ow * oh + 15) / 16 + kL3Threads / 64 - 1) / (kL3Threads / 64) <= L3Lds<N2, F3>::kUnitsPerWave);
+      lds3 <= 160 * 1024 && w3 * h3 <= kL3MaxOut &&
+      ((ow * oh + 15) / 16 + kL3Threads / 64 - 1) / (kL3Threads / 64) <= L3Lds<N2, F3>::kUnitsPerWave;
   const int g12 = grid_for_batch(batch, SRCNN_L12_GRID);
-  const int g3 = grid_for_batch(batch, l3s_L1 > 0 ? kL3sGrid : 256);
+  const int g3 = grid_for_batch(batch, 256);
   const bool kD1c = SRCNN_D1C && N1 == 64 && N2 == 32 && F1 == 9 && d1c_fits(w, h);
   // d1c below kD1cGrid samples: each sample's chunks split into `parts`
   // ranges (work items), so the grid still fills every CU's 4 block slots
   const int nch1 = (ow * oh + 31) / 32;
   int d1c_parts = kD1c ? std::max(1, std::min({4, nch1, kD1cGrid / (int)std::max<uint32_t>(batch, 1)})) : 1;
-  if (const char* e = std::getenv("SRCNN_D1C_PARTS"))  // A/B of the small-batch split (read per call)
-    if (kD1c && std::atoi(e) > 0) d1c_parts = std::min({4, nch1, std::atoi(e)});
   while (d1c_parts > 1 && (d1c_parts - 1) * ((nch1 + d1c_parts - 1) / d1c_parts) >= nch1)
     d1c_parts--;  // every part holds at least one chunk (the kernel's DMA pipeline assumes it)
   const int gd = kD1c ? (int)std::min<size_t>((size_t)batch * d1c_parts, kD1cGrid) : grid_for_batch(batch, 512);
@@ -990,12 +977,7 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
     SRCNN_LAUNCH_TRY();
   }
   L3Geom lg{(int)w, (int)h, ow, oh, w3, h3, (int)batch};
-  if (l3s_L1 > 0) {
-    SRCNN_PROFILE("l3_delta_fused", s);
-    hipLaunchKernelGGL((l3s_kernel<F3>), dim3(g3), dim3(kL3sThreads), l3s_lds_bytes(), s, A2, T, W3, B3, D2,
-                       slab3, sqs, A3, lg, l3s_L1);
-    SRCNN_LAUNCH_TRY();
-  } else if (l3_fused) {
+  if (l3_fused) {
     SRCNN_PROFILE("l3_delta_fused", s);
     int rc = launch_l3<N2, F3>(A2, T, W3, B3, D2, slab3, sqs, A3, lg, g3, lds3, s);
     if (rc) return rc;
@@ -1062,8 +1044,8 @@ static int preload_one(const srcnn_net* net) {
     return 0;
   const void* k[] = {(const void*)l12_fwd_kernel<N1, N2, F1>, (const void*)l3_delta_kernel<N2, F3>,
                      (const void*)d1_grad12_kernel<N1, N2, F1>, (const void*)slab_reduce_kernel,
-                     (const void*)d1c_grad12_kernel<9>, (const void*)l3s_kernel<5>};
-  int rc = resolve_kernels(k, SRCNN_D1C && N1 == 64 && N2 == 32 && F1 == 9 ? (F3 == 5 ? 6 : 5) : 4);
+                     (const void*)d1c_grad12_kernel<9>};
+  int rc = resolve_kernels(k, SRCNN_D1C && N1 == 64 && N2 == 32 && F1 == 9 ? 5 : 4);
   return rc ? rc : 1;
 }
 
@@ -1139,12 +1121,6 @@ extern "C" __attribute__((visibility("default"))) int srcnn_debug_d1_timing(unsi
 }
 #endif
 #ifdef SRCNN_L3_TIMING
-extern "C" __attribute__((visibility("default"))) int srcnn_debug_l3s_timing(unsigned long long* out) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(srcnn::fused::g_l3s_timing), sizeof(srcnn::fused::g_l3s_timing)) ==
-                 hipSuccess
-             ? 0
-             : -1;
-}
 extern "C" __attribute__((visibility("default"))) int srcnn_debug_l3_timing(unsigned long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(srcnn::fused::g_l3_timing), sizeof(srcnn::fused::g_l3_timing)) ==
                  hipSuccess

@@ -520,16 +520,13 @@ def test_train_step_nonsquare_tiles(S, w, h, batch):
         assert_close(got[sl], rg[sl], RTOL, "grad " + nm, xg[sl], FLIP_FLOOR)
 
 
-@pytest.mark.parametrize("l3", ["stream", "tile"])
-@pytest.mark.parametrize("batch,w,h", [(16, 33, 33), (512, 33, 33), (769, 33, 33), (7, 35, 31), (3, 39, 39),
+@pytest.mark.parametrize("batch,w,h", [(16, 33, 33), (512, 33, 33), (257, 33, 33), (7, 35, 31), (3, 39, 39),
                                        (2, 21, 21)])
-def test_train_step_l3_kernels_vs_oracle(S, monkeypatch, l3, batch, w, h):
-    """Layer 3 of the fused step on both kernels: the whole-tile
-    l3_delta_kernel (SRCNN_L3=tile, the default) and the unit-stream
-    l3s_kernel (SRCNN_L3=stream: 768 resident blocks, a ragged last round at
-    769 tiles), gradients, squared error and A3 against the oracle
-    (last_layer_delta.cl, layer_deltas.cl, backpropagate.cl)."""
-    monkeypatch.setenv("SRCNN_L3", l3)
+def test_train_step_sq_err_and_a3_vs_oracle(S, batch, w, h):
+    """The fused step's layer 3 (l3_delta_kernel): gradients, squared error
+    and the A3 it leaves in the workspace (srcnn_train_activations) against
+    the oracle (last_layer_delta.cl, squared_error.cl, layer_deltas.cl,
+    backpropagate.cl)."""
     cfg = NETS["default"]
     net = S.Net(*cfg)
     rng = np.random.default_rng(31)
@@ -548,18 +545,17 @@ def test_train_step_l3_kernels_vs_oracle(S, monkeypatch, l3, batch, w, h):
     off = S.net_offsets(net) + [P]
     for i, nm in enumerate(["W1", "B1", "W2", "B2", "W3", "B3"]):
         sl = slice(off[i], off[i + 1])
-        assert_close(got[sl], rg[sl], RTOL, "l3 %s grad %s" % (l3, nm), xg[sl], FLIP_FLOOR)
+        assert_close(got[sl], rg[sl], RTOL, "l3 grad %s" % nm, xg[sl], FLIP_FLOOR)
     pad = cfg[2] + cfg[3] + cfg[4] - 3
     A3 = orc.forward(cfg, X, w, h, batch, params)
     ref_err = orc.sq_err(T, A3, w, h, w - pad, h - pad, batch)
     assert float(H(err)[0]) == pytest.approx(ref_err, rel=1e-4)
-    # A3 as left in the workspace (srcnn_train_activations)
     n1, n2 = cfg[0], cfg[1]
     w1, h1 = w - cfg[2] + 1, h - cfg[2] + 1
     w3, h3 = w1 - cfg[4] + 1, h1 - cfg[4] + 1
     A1d, A2d, A3d = zeros(batch * w1 * h1 * n1), zeros(batch * w1 * h1 * n2), zeros(batch * w3 * h3)
     S.train_activations(net, w, h, batch, ws, nbytes, A1d, A2d, A3d)
-    assert_close(H(A3d), A3, RTOL, "l3 %s A3" % l3)
+    assert_close(H(A3d), A3, RTOL, "l3 A3")
 
 
 def test_forward_vs_oracle(S, path):
