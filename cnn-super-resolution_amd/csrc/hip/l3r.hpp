@@ -1,0 +1,410 @@
+// l3r.hpp -- fused kernel 2 of train_fused.hip for n2 = 32 (round 4; included
+// inside namespace srcnn::fused after l3_delta.hpp).  Same mathematics and
+// outputs as l3_delta_kernel:
+//   L3 forward       layer_uber_kernel.cl:70-91 (SKIP_RELU), Q trick
+//   last delta       last_layer_delta.cl:34-48 (relu' quirk on a linear layer)
+//   squared error    squared_error.cl:60-69
+//   delta2           layer_deltas.cl:79-123, MFMA over the f3*f3 taps
+//   gW3 / gB3        backpropagate.cl:89-112, MFMA over the A2 pixels
+// but with the sample's A2 tile held in REGISTERS instead of an LDS image.
+//
+// Why: l3_delta keeps two 80 KB A2 images in LDS (this sample's and the next
+// one's, filled by DMA), so it runs one block per CU and its three
+// barrier-separated phases (Q MFMAs, window sums, delta2/gW3 MFMAs) never
+// overlap anything: 0.47 of its HBM roof.  Every A2 access of the kernel is
+// per pixel except gW3's B operand (K = pixels), so A2 need not be in LDS at
+// all:
+//   - lane (lq, lg) of the wave owning 16-pixel unit u holds pixel 16u + lq,
+//     channels [4lg, 4lg+4) and [16+4lg, 16+4lg+4) (two 16-B loads);
+//   - those eight registers are the A operand of Q = A2 . W3^T (k-step s
+//     <-> channel chan(s, lg)) AND, in the delta2 phase, exactly the relu'
+//     mask of the transposed delta2 tile the same lane holds;
+//   - gW3's B operand is made per unit through a 2.5 KB per-wave transpose
+//     scratch (eight ds_write_b32, two ds_read_b128), aliased onto the Q image
+//     that the window sums have consumed by then.
+// LDS is then the Q image (62.5 KB), W3 as the Q B operand image (3.6 KB) and
+// the delta3 grid: 70 KB, so TWO blocks share a CU and one block's barrier
+// phases run under the other's MFMAs.  A2 of the block's next sample is
+// loaded into the same registers unit by unit as the delta2 phase releases
+// them, so the loads overlap the delta2 / gW3 MFMAs and the window sums.
+//
+// n2 = 32 and tiles of up to 40 16-pixel units (625-pixel A2: 33x33 samples
+// at f1 = 9); other shapes keep l3_delta_kernel.
+#ifndef SRCNN_L3R
+#define SRCNN_L3R 0  // opt-in until measured on the GPU
+#endif
+
+constexpr int kL3RThreads = 512;
+constexpr int kL3RUnits = 5;  // 16-pixel units per wave (8 waves: 640 pixels)
+constexpr int kL3RTPF = 2;    // L3 outputs per thread (w3 * h3 <= 1024)
+constexpr int kL3RW3S = 36;   // W3 image row stride (floats): conflict-free 16-B reads
+constexpr int kL3RScS = 20;   // transpose scratch row stride (floats) per channel
+
+constexpr int kL3RWdS = 36;   // delta2 W3 image row stride (floats): 4 groups x 8 slots + pad
+
+// delta2 k-slot (s, lg) -> tap, chosen so that the delta3 window offset of a
+// slot is a per-lane base plus an immediate: for s < F3, lane group lg takes
+// tap row dy = lg, dx = s; f3 = 5 puts row 4 in slots s = 5, 6 (dx = 4(s-5) + lg).
+// -1: an unused slot (zero weight).
+template <int F3>
+__host__ __device__ constexpr int l3r_tap(int s, int lg) {
+  return s < F3 ? (lg < F3 ? lg * F3 + s : -1)
+                : (F3 == 5 && s < 7 && 4 * (s - 5) + lg < 5 ? 20 + 4 * (s - 5) + lg : -1);
+}
+template <int F3>
+constexpr int l3r_kt() { return F3 == 5 ? 7 : F3; }
+
+template <int F3>
+struct L3RLds {
+  int qreg;   // Q image [16 * nunit][F3^2]; aliased by the transpose scratch and the final reduction
+  int w3img;  // W3 image [tap][kL3RW3S] (Q's B operand)
+  int wdimg;  // W3 image [c][lg][slot] at row stride kL3RWdS (delta2's A operand)
+  int d3off;  // delta3 grid offset (F3-1) * (w2 + 1)
+  int nd3;    // delta3 grid size, after a 4-float zero lead (unused slots read below the grid)
+  __host__ __device__ L3RLds(int w2, int h2) {
+    const int npx2 = w2 * h2, nunit = (npx2 + 15) / 16;
+    int r = nunit * 16 * F3 * F3;
+    if (r < 8 * 32 * kL3RScS) r = 8 * 32 * kL3RScS;
+    if (r < 2 * 2 * 4 * 64) r = 2 * 2 * 4 * 64;
+    qreg = (r + 3) & ~3;
+    w3img = (F3 * F3 * kL3RW3S + 3) & ~3;
+    wdimg = 32 * kL3RWdS;
+    d3off = (F3 - 1) * (w2 + 1);
+    nd3 = 4 + ((nunit * 16 + d3off + 4 + 3) & ~3);
+  }
+  __host__ __device__ size_t bytes() const { return ((size_t)qreg + w3img + wdimg + nd3) * sizeof(float); }
+};
+
+// the shapes l3r takes: two blocks per CU, whole units per wave
+template <int F3>
+static bool l3r_fits(int w2, int h2, int w3, int h3) {
+  const int nunit = (w2 * h2 + 15) / 16;
+  return nunit <= 8 * kL3RUnits && w3 * h3 <= kL3RThreads * kL3RTPF &&
+         L3RLds<F3>(w2, h2).bytes() <= 80 * 1024;
+}
+
+// 1: the next sample's A2 loads are issued in the delta2 phase as each unit's
+// registers free up; 0: all at the sample top (A/B)
+#ifndef SRCNN_L3R_PF
+#define SRCNN_L3R_PF 1
+#endif
+#ifndef SRCNN_L3R_WAVES
+#define SRCNN_L3R_WAVES 4  // waves per SIMD: two 8-wave blocks per CU (128 VGPRs)
+#endif
+
+template <int F3>
+__global__ __launch_bounds__(kL3RThreads, SRCNN_L3R_WAVES) void l3r_delta_kernel(
+    const float* __restrict__ A2, const float* __restrict__ T, const float* __restrict__ W3,
+    const float* __restrict__ B3, float* __restrict__ D2, float* __restrict__ slab3,
+    float* __restrict__ sq_slab, float* __restrict__ A3out, L3Geom g) {
+  constexpr int N2 = 32;
+  constexpr int K3 = F3 * F3;
+  constexpr int TT = (K3 + 15) / 16;  // 16-wide tap tiles
+  constexpr int NT = 2;               // 16-wide channel tiles
+  constexpr int KT = l3r_kt<F3>();    // delta2 k-steps (over tap slots)
+  constexpr int NW3 = K3 * N2;        // gW3 size; slab row = NW3 + 1 (gB3)
+  constexpr int nwaves = kL3RThreads / 64;
+  static_assert(K3 <= 32, "taps must fit two 16-wide MFMA tiles");
+  SRCNN_CLOCK_BEGIN();
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int npx2 = g.w2 * g.h2;
+  const int nunit = (npx2 + 15) / 16;
+  const L3RLds<F3> L(g.w2, g.h2);
+  const int d3off = L.d3off;
+  float* qs = smem;                        // Q[q][tap]
+  float* w3s = smem + L.qreg;              // W3[tap][c] at row stride kL3RW3S
+  float* wds = w3s + L.w3img;              // W3[tap(s, lg)][c] at c * kL3RWdS + 8 lg + s
+  float* d3g = wds + L.wdimg + 4;          // delta3 on the A2 grid (l3_delta.hpp)
+  float* red = smem;                       // end-of-kernel reduction scratch
+
+  const int tid = threadIdx.x;
+  const int lane = mfma::lane_id(), wave = mfma::wave_id();
+  const int lq = lane & 15, lg = lane >> 4;
+  const int pad = (g.W - g.w3) / 2;  // last_layer_delta.cl:25
+  const int nout = g.w3 * g.h3;
+
+  for (int i = tid - 4; i < L.nd3 - 4; i += kL3RThreads) d3g[i] = 0.0f;
+  for (int i = tid; i < K3 * N2; i += kL3RThreads) w3s[(i / N2) * kL3RW3S + i % N2] = W3[i];
+  for (int i = tid; i < 32 * 32; i += kL3RThreads) {
+    const int c = i >> 5, gs = i & 31, tap = l3r_tap<F3>(gs & 7, gs >> 3);
+    wds[c * kL3RWdS + gs] = (gs & 7) < KT && tap >= 0 ? W3[tap * N2 + c] : 0.0f;
+  }
+
+  auto tap_off = [&](int tap) { return tap < K3 ? (tap / F3) * g.w2 + tap % F3 : 0; };
+  const float b3 = B3[0];
+  // delta2^T B operand, pixel u0 + lq, slot (s, lg): delta3 at
+  //   d3b0 - s            (s < F3: tap row lg, dx = s)
+  //   d3b1 - 4 (s - 5)    (f3 = 5, s = 5, 6: tap row 4, dx = 4(s-5) + lg)
+  // unused slots read finite values (zero weight); lanes past the tap rows
+  // (f3 = 3, lg = 3) read row 0's windows
+  const int d3b0 = lq + d3off - (lg < F3 ? lg : 0) * g.w2;
+  const int d3b1 = lq + d3off - (F3 - 1) * g.w2 - lg;
+  //  goff[t]: delta3 window of tap 16t + lq (gW3 A operand; lanes past the
+  //           taps read a real window: their gW3 rows are discarded)
+  int goff[TT];
+#pragma unroll
+  for (int t = 0; t < TT; t++) goff[t] = d3off - tap_off(16 * t + lq);
+  // per-lane LDS bases of this wave's units (unit j adds the immediate 128 j;
+  // LDS offsets are unsigned, so the bases sit at the lowest address read)
+  int adb0 = d3b0 - (F3 - 1) + 16 * wave, adb1 = d3b1 - 4 + 16 * wave, agb[TT];
+  asm volatile("" : "+v"(adb0), "+v"(adb1));
+#pragma unroll
+  for (int t = 0; t < TT; t++) {
+    agb[t] = goff[t] + 4 * lg + 16 * wave;
+    asm volatile("" : "+v"(agb[t]));
+  }
+  // delta2^T A operand W3[tap(s, lg)][16t + lq]: two 16-B reads per channel tile
+  const int wdo = lq * kL3RWdS + 8 * lg;
+  // Q B operand W3[tap 16t + lq][chan(s, lg)] with chan(s, lg) = 4lg + s for
+  // s < 4 and 16 + 4lg + s - 4 above: two 16-B reads per tap tile
+  const int wqo = lq * kL3RW3S + 4 * lg;
+  // transpose scratch of this wave (channel-major, row stride kL3RScS):
+  // written as channel 4lg + i (+16) of pixel lq, read as pixels 4lg..4lg+3
+  // of channel 16t + lq (one 16-B read per channel tile)
+  float* scw = smem + wave * (32 * kL3RScS);
+  const int sco_w = 4 * lg * kL3RScS + lq, sco_r = lq * kL3RScS + 4 * lg;
+
+  f32x4 gacc[TT][NT];
+#pragma unroll
+  for (int t3 = 0; t3 < TT; t3++)
+#pragma unroll
+    for (int t = 0; t < NT; t++) gacc[t3][t] = mfma::zero4();
+  float gb3 = 0.0f, sq = 0.0f;
+
+  // this lane's A2 registers: unit j = wave + 8j, pixel 16u + lq, channel
+  // quads lg and 4 + lg (zeros past the sample)
+  f32x4 a2r[kL3RUnits][2];
+  // (addresses: a wave-uniform base + one 32-bit lane offset, re-formed at
+  // each use; precomputed 64-bit pointers per unit cost registers)
+  const int a2lo = lq * N2 + 4 * lg;
+#define SRCNN_L3R_LOAD(J, SAMPLE)                                                       \
+  do {                                                                                  \
+    const int q_ = 16 * (wave + nwaves * (J)) + lq;                                     \
+    if (q_ < npx2) {                                                                    \
+      const float* b_ = A2 + ((size_t)(SAMPLE)*npx2 + 16 * wave) * N2;                  \
+      int o_ = a2lo + 16 * nwaves * N2 * (J);                                           \
+      asm volatile("" : "+v"(o_));                                                      \
+      a2r[J][0] = *reinterpret_cast<const f32x4*>(b_ + o_);                             \
+      a2r[J][1] = *reinterpret_cast<const f32x4*>(b_ + o_ + 16);                        \
+    } else {                                                                            \
+      a2r[J][0] = mfma::zero4();                                                        \
+      a2r[J][1] = mfma::zero4();                                                        \
+    }                                                                                   \
+  } while (0)
+
+  // ground truth of this thread's L3 outputs, prefetched one sample ahead
+  // (tof: the output's offset in its sample, -1 past the outputs)
+  int tof[kL3RTPF];
+#pragma unroll
+  for (int k = 0; k < kL3RTPF; k++) {
+    const int t_ = tid + k * kL3RThreads;
+    const int y_ = t_ / g.w3, x_ = t_ - y_ * g.w3;
+    tof[k] = t_ < nout ? (y_ + pad) * g.W + x_ + pad : -1;
+  }
+  float tpf[kL3RTPF];
+#define SRCNN_L3R_T_PREFETCH(SAMPLE)                                                   \
+  do {                                                                                 \
+    const float* b_ = T + (size_t)(SAMPLE)*g.W * g.H;                                  \
+    _Pragma("unroll") for (int k = 0; k < kL3RTPF; k++) tpf[k] = tof[k] >= 0 ? b_[tof[k]] : 0.f; \
+  } while (0)
+
+  if ((int)blockIdx.x < g.batch) {
+    const int s0 = l3_order(blockIdx.x, g.batch);
+#pragma unroll
+    for (int j = 0; j < kL3RUnits; j++) SRCNN_L3R_LOAD(j, s0);
+    SRCNN_L3R_T_PREFETCH(s0);
+  }
+
+  for (int sample = blockIdx.x; sample < g.batch; sample += gridDim.x) {
+    // the previous sample's readers of the transpose scratch (= Q image) and
+    // of the delta3 grid are done; a bare barrier: the next sample's A2
+    // loads and this sample's D2 stores stay in flight
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const int smp = l3_order(sample, g.batch);
+    float tcur[kL3RTPF];
+#pragma unroll
+    for (int k = 0; k < kL3RTPF; k++) tcur[k] = tpf[k];
+    const int next = sample + (int)gridDim.x;
+    const bool has_next = next < g.batch;
+    const int nsmp = has_next ? l3_order(next, g.batch) : smp;
+    if (has_next) SRCNN_L3R_T_PREFETCH(nsmp);
+    if (!SRCNN_L3R_PF && sample != (int)blockIdx.x) {
+#pragma unroll
+      for (int j = 0; j < kL3RUnits; j++) SRCNN_L3R_LOAD(j, smp);
+    }
+
+    // ---- Q = A2 . W3^T per 16-pixel unit, A operand from registers ----
+#pragma unroll
+    for (int j = 0; j < kL3RUnits; j++) {
+      const int u = wave + nwaves * j;
+      if (u < nunit) {
+        const int u0 = 16 * u;
+        f32x4 wv[TT][2];
+#pragma unroll
+        for (int t = 0; t < TT; t++)
+#pragma unroll
+          for (int h = 0; h < 2; h++)
+            wv[t][h] = *reinterpret_cast<const f32x4*>(w3s + wqo + 16 * t * kL3RW3S + 16 * h);
+        f32x4 acc[TT];
+#pragma unroll
+        for (int t = 0; t < TT; t++) acc[t] = mfma::zero4();
+#pragma unroll
+        for (int s = 0; s < 8; s++)
+#pragma unroll
+          for (int t = 0; t < TT; t++) acc[t] = mfma::mma16(a2r[j][s >> 2][s & 3], wv[t][s >> 2][s & 3], acc[t]);
+        // Q[u0 + 4lg + i][tap = 16t + lq] (rows past the sample are written
+        // too, never read)
+#pragma unroll
+        for (int t = 0; t < TT; t++) {
+          const int tap = 16 * t + lq;
+          if (tap < K3) {
+            float* qd = qs + (u0 + 4 * lg) * K3 + tap;
+#pragma unroll
+            for (int i = 0; i < 4; i++) qd[i * K3] = acc[t][i];
+          }
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+
+    // ---- L3 = B3 + diagonal sums of Q; last delta; squared error ----
+#pragma unroll
+    for (int k = 0; k < kL3RTPF; k++) {
+      const int t = tid + k * kL3RThreads;
+      if (t < nout) {
+        const int y = t / g.w3, x = t - y * g.w3;
+        const float* qrow = qs + (y * g.w2 + x) * K3;
+        float acc = 0.0f;
+#pragma unroll
+        for (int dy = 0; dy < F3; dy++)
+#pragma unroll
+          for (int dx = 0; dx < F3; dx++) acc += qrow[(dy * g.w2 + dx) * K3 + dy * F3 + dx];
+        const float a3 = acc + b3;
+        A3out[(size_t)smp * nout + t] = a3;
+        const float diff = a3 - tcur[k];
+        const float d3 = diff * (a3 > 0.0f ? 1.0f : 0.0f);
+        d3g[y * g.w2 + x + d3off] = d3;
+        gb3 += d3;
+        sq += diff * diff;
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+
+    // ---- per 16-pixel unit: delta2 and gW3 MFMAs ----
+    //   delta2[q][n] = [A2 > 0] * sum_tap delta3(q - off(tap)) W3[tap][n]
+    //   gW3[tap][n] += sum_p delta3(p - off(tap)) A2[p][n]
+    // delta2 runs transposed (M = channels, N = pixels): C register i of lane
+    // (lq, lg) in tile t is delta2[u0 + lq][16t + 4lg + i], whose relu' mask
+    // is a2r[j][t][i].  Then this unit's registers take the next sample's A2.
+    float* d2s = D2 + ((size_t)smp * npx2 + 16 * wave) * N2;
+#pragma unroll
+    for (int j = 0; j < kL3RUnits; j++) {
+      const int u = wave + nwaves * j;
+      if (u < nunit) {
+        const int u0 = 16 * u;
+        // gW3's B operand A2[u0 + 4lg + s][16t + lq] through the scratch
+#pragma unroll
+        for (int h = 0; h < 2; h++)
+#pragma unroll
+          for (int i = 0; i < 4; i++) scw[sco_w + (16 * h + i) * kL3RScS] = a2r[j][h][i];
+        float ad[KT], ag[4][TT];
+#pragma unroll
+        for (int s = 0; s < KT; s++)
+          ad[s] = s < F3 ? d3g[adb0 + 128 * j + (F3 - 1 - s)] : d3g[adb1 + 128 * j + 4 * (6 - s)];
+        f32x4 wv[NT][2];
+#pragma unroll
+        for (int t = 0; t < NT; t++)
+#pragma unroll
+          for (int h = 0; h < 2; h++)
+            wv[t][h] = *reinterpret_cast<const f32x4*>(wds + wdo + 16 * t * kL3RWdS + 4 * h);
+#pragma unroll
+        for (int s = 0; s < 4; s++)
+#pragma unroll
+          for (int t3 = 0; t3 < TT; t3++) ag[s][t3] = d3g[agb[t3] + 128 * j + s];
+        f32x4 bg[NT];
+#pragma unroll
+        for (int t = 0; t < NT; t++) bg[t] = *reinterpret_cast<const f32x4*>(scw + sco_r + 16 * t * kL3RScS);
+        f32x4 acc[NT];
+#pragma unroll
+        for (int t = 0; t < NT; t++) acc[t] = mfma::zero4();
+#pragma unroll
+        for (int s = 0; s < KT; s++)
+#pragma unroll
+          for (int t = 0; t < NT; t++) acc[t] = mfma::mma16(wv[t][s >> 2][s & 3], ad[s], acc[t]);
+#pragma unroll
+        for (int s = 0; s < 4; s++)
+#pragma unroll
+          for (int t3 = 0; t3 < TT; t3++)
+#pragma unroll
+            for (int t = 0; t < NT; t++) gacc[t3][t] = mfma::mma16(ag[s][t3], bg[t][s], gacc[t3][t]);
+        const int q = u0 + lq;
+        if (q < npx2) {
+          int o_ = a2lo + 16 * nwaves * N2 * j;
+          asm volatile("" : "+v"(o_));
+          float* dst = d2s + o_;
+#pragma unroll
+          for (int t = 0; t < NT; t++) {
+            f32x4 v;
+#pragma unroll
+            for (int i = 0; i < 4; i++) v[i] = a2r[j][t][i] > 0.0f ? acc[t][i] : 0.0f;
+            *reinterpret_cast<f32x4*>(dst + 16 * t) = v;
+          }
+        }
+        if (SRCNN_L3R_PF && has_next) SRCNN_L3R_LOAD(j, nsmp);
+      }
+    }
+  }
+#undef SRCNN_L3R_LOAD
+#undef SRCNN_L3R_T_PREFETCH
+  SRCNN_CLOCK_END(g_clk, 1);
+
+  // ---- block reduction of the partial gradients, waves in order ----
+  __syncthreads();
+  for (int w = 0; w < nwaves; w++) {
+    if (wave == w) {
+#pragma unroll
+      for (int t3 = 0; t3 < TT; t3++)
+#pragma unroll
+        for (int t = 0; t < NT; t++)
+#pragma unroll
+          for (int i = 0; i < 4; i++) {
+            float* dst = red + ((t3 * NT + t) * 4 + i) * 64 + lane;
+            *dst = (w == 0 ? 0.0f : *dst) + gacc[t3][t][i];
+          }
+    }
+    __syncthreads();
+  }
+  float* out = slab3 + (size_t)blockIdx.x * (NW3 + 1);
+  for (int i = tid; i < TT * NT * 4 * 64; i += kL3RThreads) {
+    const int k = i >> 8, r = (i >> 6) & 3, l = i & 63;
+    const int t3 = k / NT, t = k - t3 * NT;
+    const int tap = 16 * t3 + 4 * (l >> 4) + r, n = 16 * t + (l & 15);
+    if (tap < K3) out[tap * N2 + n] = red[i];
+  }
+  // gB3 and squared error: per-wave shuffle trees, then waves in order
+  for (int off = 32; off > 0; off >>= 1) {
+    gb3 += __shfl_down(gb3, off, 64);
+    sq += __shfl_down(sq, off, 64);
+  }
+  __syncthreads();
+  if (lane == 0) {
+    red[2 * wave] = gb3;
+    red[2 * wave + 1] = sq;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    float tb = 0.f, ts = 0.f;
+    for (int w = 0; w < nwaves; w++) {
+      tb += red[2 * w];
+      ts += red[2 * w + 1];
+    }
+    out[NW3] = tb;
+    sq_slab[blockIdx.x] = ts;
+  }
+}

@@ -283,6 +283,7 @@ __global__ __launch_bounds__(256, SRCNN_L12_WAVES) void l12_fwd_kernel(
 #undef SRCNN_W1F
 
 #include "l3_delta.hpp"
+#include "l3r.hpp"
 
 #ifdef SRCNN_D1_TIMING
 // diagnostics build only: wave 0's cycles per section of the chunk loop
@@ -898,6 +899,21 @@ struct Net {
 
 static int grid_for_batch(uint32_t batch, int cap) { return (int)std::min<uint32_t>(batch, cap); }
 
+template <int F3>
+static int launch_l3r(const float* A2, const float* T, const float* W3, const float* B3, float* D2,
+                      float* slab3, float* sqs, float* A3, const L3Geom& lg, int grid, size_t lds,
+                      hipStream_t s) {
+  // 70 KB exceeds the 64 KiB default dynamic LDS (set per launch: see launch_l3)
+  hipError_t e = hipFuncSetAttribute((const void*)l3r_delta_kernel<F3>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+  if (e != hipSuccess)
+    return fail(SRCNN_ERR_HIP, "hipFuncSetAttribute(l3r_delta): %s", hipGetErrorString(e));
+  hipLaunchKernelGGL((l3r_delta_kernel<F3>), dim3(grid), dim3(kL3RThreads), lds, s, A2, T, W3, B3,
+                     D2, slab3, sqs, A3, lg);
+  SRCNN_LAUNCH_TRY();
+  return SRCNN_OK;
+}
+
 template <int N2, int F3>
 static int launch_l3(const float* A2, const float* T, const float* W3, const float* B3, float* D2,
                      float* slab3, float* sqs, float* A3, const L3Geom& lg, int grid, size_t lds,
@@ -930,12 +946,14 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   // f1 = 9).  Larger tiles (e.g. the reference's 36x36 samples, profile.py:7)
   // keep l12 and d1 and run layer 3 through the op-level kernels instead
   // (ops_fast.hip: L3 forward, last delta, delta2, gW3 over HWC A2 / A3 / D3).
-  const size_t lds3 = l3_lds_bytes<N2, F3>(ow, oh);
+  // n2 = 32: l3r (A2 in registers, two blocks per CU) where the tile fits it
+  const bool l3r = SRCNN_L3R && N2 == 32 && l3r_fits<F3>(ow, oh, w3, h3);
+  const size_t lds3 = l3r ? L3RLds<F3>(ow, oh).bytes() : l3_lds_bytes<N2, F3>(ow, oh);
   const bool l3_fused =
-      lds3 <= 160 * 1024 && w3 * h3 <= kL3MaxOut &&
-      ((ow * oh + 15) / 16 + kL3Threads / 64 - 1) / (kL3Threads / 64) <= L3Lds<N2, F3>::kUnitsPerWave;
+      l3r || (lds3 <= 160 * 1024 && w3 * h3 <= kL3MaxOut &&
+              ((ow * oh + 15) / 16 + kL3Threads / 64 - 1) / (kL3Threads / 64) <= L3Lds<N2, F3>::kUnitsPerWave);
   const int g12 = grid_for_batch(batch, SRCNN_L12_GRID);
-  const int g3 = grid_for_batch(batch, 256);
+  const int g3 = grid_for_batch(batch, l3r ? 512 : 256);
   const bool kD1c = SRCNN_D1C && N1 == 64 && N2 == 32 && F1 == 9 && d1c_fits(w, h);
   // d1c below kD1cGrid samples: each sample's chunks split into `parts`
   // ranges (work items), so the grid still fills every CU's 4 block slots
@@ -979,7 +997,8 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   L3Geom lg{(int)w, (int)h, ow, oh, w3, h3, (int)batch};
   if (l3_fused) {
     SRCNN_PROFILE("l3_delta_fused", s);
-    int rc = launch_l3<N2, F3>(A2, T, W3, B3, D2, slab3, sqs, A3, lg, g3, lds3, s);
+    int rc = l3r ? launch_l3r<F3>(A2, T, W3, B3, D2, slab3, sqs, A3, lg, g3, lds3, s)
+                 : launch_l3<N2, F3>(A2, T, W3, B3, D2, slab3, sqs, A3, lg, g3, lds3, s);
     if (rc) return rc;
   } else {
     // ConfigBasedDataPipeline.cpp:200-323 for layer 3 on the op-level kernels
@@ -1044,8 +1063,8 @@ static int preload_one(const srcnn_net* net) {
     return 0;
   const void* k[] = {(const void*)l12_fwd_kernel<N1, N2, F1>, (const void*)l3_delta_kernel<N2, F3>,
                      (const void*)d1_grad12_kernel<N1, N2, F1>, (const void*)slab_reduce_kernel,
-                     (const void*)d1c_grad12_kernel<9>};
-  int rc = resolve_kernels(k, SRCNN_D1C && N1 == 64 && N2 == 32 && F1 == 9 ? 5 : 4);
+                     (const void*)l3r_delta_kernel<F3>, (const void*)d1c_grad12_kernel<9>};
+  int rc = resolve_kernels(k, SRCNN_D1C && N1 == 64 && N2 == 32 && F1 == 9 ? 6 : 5);
   return rc ? rc : 1;
 }
 
