@@ -31,14 +31,14 @@
 // n2 = 32 and tiles of up to 40 16-pixel units (625-pixel A2: 33x33 samples
 // at f1 = 9); other shapes keep l3_delta_kernel.
 #ifndef SRCNN_L3R
-#define SRCNN_L3R 0  // opt-in until measured on the GPU
+#define SRCNN_L3R 1
 #endif
 
 constexpr int kL3RThreads = 512;
 constexpr int kL3RUnits = 5;  // 16-pixel units per wave (8 waves: 640 pixels)
-constexpr int kL3RTPF = 2;    // L3 outputs per thread (w3 * h3 <= 1024)
+constexpr int kL3RTPF = 1;    // L3 outputs per thread (w3 * h3 <= 512 for every A2 tile of <= 640 pixels)
 constexpr int kL3RW3S = 36;   // W3 image row stride (floats): conflict-free 16-B reads
-constexpr int kL3RScS = 20;   // transpose scratch row stride (floats) per channel
+constexpr int kL3RScS = 36;   // transpose scratch row stride (floats) per channel
 
 constexpr int kL3RWdS = 36;   // delta2 W3 image row stride (floats): 4 groups x 8 slots + pad
 
@@ -56,21 +56,26 @@ constexpr int l3r_kt() { return F3 == 5 ? 7 : F3; }
 
 template <int F3>
 struct L3RLds {
-  int qreg;   // Q image [16 * nunit][F3^2]; aliased by the transpose scratch and the final reduction
+  int qreg;   // Q image [640][F3^2] (every unit slot); aliased by the transpose scratch and the final reduction
   int w3img;  // W3 image [tap][kL3RW3S] (Q's B operand)
-  int wdimg;  // W3 image [c][lg][slot] at row stride kL3RWdS (delta2's A operand)
+  int wdimg;  // W3 image [c][h][lg][4] at row stride kL3RWdS (delta2's A operand; slot s = 4h + i)
   int d3off;  // delta3 grid offset (F3-1) * (w2 + 1)
   int nd3;    // delta3 grid size, after a 4-float zero lead (unused slots read below the grid)
   __host__ __device__ L3RLds(int w2, int h2) {
-    const int npx2 = w2 * h2, nunit = (npx2 + 15) / 16;
-    int r = nunit * 16 * F3 * F3;
+    // every wave runs all kL3RUnits unit slots (no data-dependent branches
+    // around the A2 loads: the compiler's wait-count pass would then lose
+    // track of them and wait for every load right after issuing it), so the
+    // Q image and the delta3 grid cover all 8 * kL3RUnits units
+    (void)h2;
+    constexpr int npad = 16 * 8 * kL3RUnits;
+    int r = npad * F3 * F3;
     if (r < 8 * 32 * kL3RScS) r = 8 * 32 * kL3RScS;
     if (r < 2 * 2 * 4 * 64) r = 2 * 2 * 4 * 64;
     qreg = (r + 3) & ~3;
     w3img = (F3 * F3 * kL3RW3S + 3) & ~3;
     wdimg = 32 * kL3RWdS;
     d3off = (F3 - 1) * (w2 + 1);
-    nd3 = 4 + ((nunit * 16 + d3off + 4 + 3) & ~3);
+    nd3 = 4 + ((npad + d3off + 4 + 3) & ~3);
   }
   __host__ __device__ size_t bytes() const { return ((size_t)qreg + w3img + wdimg + nd3) * sizeof(float); }
 };
@@ -83,11 +88,24 @@ static bool l3r_fits(int w2, int h2, int w3, int h3) {
          L3RLds<F3>(w2, h2).bytes() <= 80 * 1024;
 }
 
-// 1: the next sample's A2 loads are issued in the delta2 phase as each unit's
-// registers free up; 0: all at the sample top (A/B)
-#ifndef SRCNN_L3R_PF
-#define SRCNN_L3R_PF 1
+// diagnostics builds only (results invalid): 1 no D2 stores, 2 no next-sample
+// A2 loads, 4 no delta2 MFMAs, 8 no gW3 MFMAs, 16 no transpose scratch
+#ifndef SRCNN_L3R_DIAG
+#define SRCNN_L3R_DIAG 0
 #endif
+#ifndef SRCNN_L3R_UNIT_FENCE
+#define SRCNN_L3R_UNIT_FENCE 1
+#endif
+// D2 store cache policy (A/B): 0 default, 1 nontemporal
+#ifndef SRCNN_L3R_D2NT
+#define SRCNN_L3R_D2NT 0
+#endif
+__device__ __forceinline__ void st_d2(float* p, f32x4 v) {
+  if (SRCNN_L3R_D2NT)
+    __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p));
+  else
+    *reinterpret_cast<f32x4*>(p) = v;
+}
 #ifndef SRCNN_L3R_WAVES
 #define SRCNN_L3R_WAVES 4  // waves per SIMD: two 8-wave blocks per CU (128 VGPRs)
 #endif
@@ -108,7 +126,6 @@ __global__ __launch_bounds__(kL3RThreads, SRCNN_L3R_WAVES) void l3r_delta_kernel
   SRCNN_CLOCK_BEGIN();
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int npx2 = g.w2 * g.h2;
-  const int nunit = (npx2 + 15) / 16;
   const L3RLds<F3> L(g.w2, g.h2);
   const int d3off = L.d3off;
   float* qs = smem;                        // Q[q][tap]
@@ -127,7 +144,9 @@ __global__ __launch_bounds__(kL3RThreads, SRCNN_L3R_WAVES) void l3r_delta_kernel
   for (int i = tid; i < K3 * N2; i += kL3RThreads) w3s[(i / N2) * kL3RW3S + i % N2] = W3[i];
   for (int i = tid; i < 32 * 32; i += kL3RThreads) {
     const int c = i >> 5, gs = i & 31, tap = l3r_tap<F3>(gs & 7, gs >> 3);
-    wds[c * kL3RWdS + gs] = (gs & 7) < KT && tap >= 0 ? W3[tap * N2 + c] : 0.0f;
+    // slot s = gs & 7 of lane group lg = gs >> 3 at 16 (s >> 2) + 4 lg + (s & 3)
+    wds[c * kL3RWdS + 16 * ((gs & 7) >> 2) + 4 * (gs >> 3) + (gs & 3)] =
+        (gs & 7) < KT && tap >= 0 ? W3[tap * N2 + c] : 0.0f;
   }
 
   auto tap_off = [&](int tap) { return tap < K3 ? (tap / F3) * g.w2 + tap % F3 : 0; };
@@ -154,7 +173,7 @@ __global__ __launch_bounds__(kL3RThreads, SRCNN_L3R_WAVES) void l3r_delta_kernel
     asm volatile("" : "+v"(agb[t]));
   }
   // delta2^T A operand W3[tap(s, lg)][16t + lq]: two 16-B reads per channel tile
-  const int wdo = lq * kL3RWdS + 8 * lg;
+
   // Q B operand W3[tap 16t + lq][chan(s, lg)] with chan(s, lg) = 4lg + s for
   // s < 4 and 16 + 4lg + s - 4 above: two 16-B reads per tap tile
   const int wqo = lq * kL3RW3S + 4 * lg;
@@ -162,7 +181,14 @@ __global__ __launch_bounds__(kL3RThreads, SRCNN_L3R_WAVES) void l3r_delta_kernel
   // written as channel 4lg + i (+16) of pixel lq, read as pixels 4lg..4lg+3
   // of channel 16t + lq (one 16-B read per channel tile)
   float* scw = smem + wave * (32 * kL3RScS);
-  const int sco_w = 4 * lg * kL3RScS + lq, sco_r = lq * kL3RScS + 4 * lg;
+  // (the three images share the row stride 36, so one lane base wqo serves
+  // the Q and delta2 W3 operands and the scratch reads)
+  static_assert(kL3RW3S == kL3RWdS && kL3RW3S == kL3RScS, "shared lane base");
+  const int sco_w = 4 * lg * kL3RScS + lq;
+  // the same scratch as [pixel][kL3RScS] rows for the D2 stores: this lane's
+  // quads of pixel lq (write), whole-row quads of pixels lq & 7 (+8) (read)
+  const int srw = lq * kL3RScS + 4 * lg;
+  const int srr = (lq & 7) * kL3RScS + 4 * (lg + 4 * (lq >> 3));
 
   f32x4 gacc[TT][NT];
 #pragma unroll
@@ -172,23 +198,42 @@ __global__ __launch_bounds__(kL3RThreads, SRCNN_L3R_WAVES) void l3r_delta_kernel
   float gb3 = 0.0f, sq = 0.0f;
 
   // this lane's A2 registers: unit j = wave + 8j, pixel 16u + lq, channel
-  // quads lg and 4 + lg (zeros past the sample)
+  // quads lg and 4 + lg.  Past the sample's pixels a lane loads pixel lq
+  // instead (finite values; no branch): such pixels' Q rows are never read,
+  // their delta2 is not stored, and their delta3 windows lie past every
+  // written delta3 (index >= npx2 in the zeroed grid), so they add exactly 0
+  // to gW3
   f32x4 a2r[kL3RUnits][2];
   // (addresses: a wave-uniform base + one 32-bit lane offset, re-formed at
   // each use; precomputed 64-bit pointers per unit cost registers)
-  const int a2lo = lq * N2 + 4 * lg;
+  // (A2 loads / D2 stores: pixel lq & 7, quad lg (lq < 8) or 4 + lg of the row)
+  const bool lo8 = lq < 8;
 #define SRCNN_L3R_LOAD(J, SAMPLE)                                                       \
   do {                                                                                  \
-    const int q_ = 16 * (wave + nwaves * (J)) + lq;                                     \
-    if (q_ < npx2) {                                                                    \
-      const float* b_ = A2 + ((size_t)(SAMPLE)*npx2 + 16 * wave) * N2;                  \
-      int o_ = a2lo + 16 * nwaves * N2 * (J);                                           \
-      asm volatile("" : "+v"(o_));                                                      \
-      a2r[J][0] = *reinterpret_cast<const f32x4*>(b_ + o_);                             \
-      a2r[J][1] = *reinterpret_cast<const f32x4*>(b_ + o_ + 16);                        \
-    } else {                                                                            \
-      a2r[J][0] = mfma::zero4();                                                        \
-      a2r[J][1] = mfma::zero4();                                                        \
+    /* formed here from an opaque lane id: hoisted out of the sample loop,  */          \
+    /* the ten per-unit offsets would be held (spilled) across it           */          \
+    int l_ = lane;                                                                      \
+    asm volatile("" : "+v"(l_));                                                        \
+    const int lo_ = ((l_ & 7) * N2 + 4 * ((l_ >> 4) + 4 * ((l_ >> 3) & 1)));            \
+    const int pa_ = 16 * (wave + nwaves * (J)) + (l_ & 7);                              \
+    const float* b_ = A2 + (size_t)(SAMPLE)*npx2 * N2;                                  \
+    const unsigned w_ = 16 * (wave + nwaves * (J)) * N2 + lo_;                          \
+    const unsigned oa_ = pa_ < npx2 ? w_ : lo_; /* else pixel lq & 7 of the sample */   \
+    const unsigned ob_ = pa_ + 8 < npx2 ? w_ + 8 * N2 : lo_;                            \
+    a2r[J][0] = *reinterpret_cast<const f32x4*>(b_ + oa_);                              \
+    a2r[J][1] = *reinterpret_cast<const f32x4*>(b_ + ob_);                              \
+  } while (0)
+  // loaded as whole 128-B pixel rows (store A / B of the D2 layout below);
+  // at first use the lanes lq, lq ^ 8 swap one quad so that lane (lq, lg)
+  // holds quads lg and 4 + lg of pixel lq
+#define SRCNN_L3R_SWAP(J)                                                               \
+  do {                                                                                  \
+    _Pragma("unroll") for (int i_ = 0; i_ < 4; i_++) {                                  \
+      const float a_ = a2r[J][0][i_], b_ = a2r[J][1][i_];                               \
+      const float r_ = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(               \
+          __builtin_bit_cast(int, lo8 ? b_ : a_), 0x128, 0xF, 0xF, false));              \
+      a2r[J][0][i_] = lo8 ? a_ : r_;                                                    \
+      a2r[J][1][i_] = lo8 ? r_ : b_;                                                    \
     }                                                                                   \
   } while (0)
 
@@ -205,7 +250,10 @@ __global__ __launch_bounds__(kL3RThreads, SRCNN_L3R_WAVES) void l3r_delta_kernel
 #define SRCNN_L3R_T_PREFETCH(SAMPLE)                                                   \
   do {                                                                                 \
     const float* b_ = T + (size_t)(SAMPLE)*g.W * g.H;                                  \
-    _Pragma("unroll") for (int k = 0; k < kL3RTPF; k++) tpf[k] = tof[k] >= 0 ? b_[tof[k]] : 0.f; \
+    _Pragma("unroll") for (int k = 0; k < kL3RTPF; k++) {                              \
+      const float x_ = b_[tof[k] >= 0 ? tof[k] : 0];                                   \
+      tpf[k] = tof[k] >= 0 ? x_ : 0.f;                                                 \
+    }                                                                                  \
   } while (0)
 
   if ((int)blockIdx.x < g.batch) {
@@ -215,6 +263,9 @@ __global__ __launch_bounds__(kL3RThreads, SRCNN_L3R_WAVES) void l3r_delta_kernel
     SRCNN_L3R_T_PREFETCH(s0);
   }
 
+#ifdef SRCNN_L3_TIMING
+  unsigned long long tacc[4] = {0, 0, 0, 0}, tlast = clock64();
+#endif
   for (int sample = blockIdx.x; sample < g.batch; sample += gridDim.x) {
     // the previous sample's readers of the transpose scratch (= Q image) and
     // of the delta3 grid are done; a bare barrier: the next sample's A2
@@ -222,6 +273,7 @@ __global__ __launch_bounds__(kL3RThreads, SRCNN_L3R_WAVES) void l3r_delta_kernel
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    SRCNN_L3_TICK(0);
     const int smp = l3_order(sample, g.batch);
     float tcur[kL3RTPF];
 #pragma unroll
@@ -229,18 +281,16 @@ __global__ __launch_bounds__(kL3RThreads, SRCNN_L3R_WAVES) void l3r_delta_kernel
     const int next = sample + (int)gridDim.x;
     const bool has_next = next < g.batch;
     const int nsmp = has_next ? l3_order(next, g.batch) : smp;
-    if (has_next) SRCNN_L3R_T_PREFETCH(nsmp);
-    if (!SRCNN_L3R_PF && sample != (int)blockIdx.x) {
-#pragma unroll
-      for (int j = 0; j < kL3RUnits; j++) SRCNN_L3R_LOAD(j, smp);
-    }
+    SRCNN_L3R_T_PREFETCH(nsmp);  // (a harmless re-read without a next sample)
 
     // ---- Q = A2 . W3^T per 16-pixel unit, A operand from registers ----
 #pragma unroll
     for (int j = 0; j < kL3RUnits; j++) {
+      if (SRCNN_L3R_UNIT_FENCE) __builtin_amdgcn_sched_barrier(0);  // no operand motion across units (registers)
       const int u = wave + nwaves * j;
-      if (u < nunit) {
+      {  // every slot, also past the sample's units (zero A2, stores masked)
         const int u0 = 16 * u;
+        SRCNN_L3R_SWAP(j);
         f32x4 wv[TT][2];
 #pragma unroll
         for (int t = 0; t < TT; t++)
@@ -270,6 +320,7 @@ __global__ __launch_bounds__(kL3RThreads, SRCNN_L3R_WAVES) void l3r_delta_kernel
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    SRCNN_L3_TICK(1);
 
     // ---- L3 = B3 + diagonal sums of Q; last delta; squared error ----
 #pragma unroll
@@ -295,6 +346,7 @@ __global__ __launch_bounds__(kL3RThreads, SRCNN_L3R_WAVES) void l3r_delta_kernel
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    SRCNN_L3_TICK(2);
 
     // ---- per 16-pixel unit: delta2 and gW3 MFMAs ----
     //   delta2[q][n] = [A2 > 0] * sum_tap delta3(q - off(tap)) W3[tap][n]
@@ -305,15 +357,14 @@ __global__ __launch_bounds__(kL3RThreads, SRCNN_L3R_WAVES) void l3r_delta_kernel
     float* d2s = D2 + ((size_t)smp * npx2 + 16 * wave) * N2;
 #pragma unroll
     for (int j = 0; j < kL3RUnits; j++) {
+      if (SRCNN_L3R_UNIT_FENCE) __builtin_amdgcn_sched_barrier(0);  // no operand motion across units (registers)
       const int u = wave + nwaves * j;
-      if (u < nunit) {
+      {  // every slot, also past the sample's units (zero A2, stores masked)
         const int u0 = 16 * u;
-        // gW3's B operand A2[u0 + 4lg + s][16t + lq] through the scratch
-#pragma unroll
-        for (int h = 0; h < 2; h++)
-#pragma unroll
-          for (int i = 0; i < 4; i++) scw[sco_w + (16 * h + i) * kL3RScS] = a2r[j][h][i];
-        float ad[KT], ag[4][TT];
+        // delta2, its masked stores, then gW3, fenced apart so that the
+        // groups' operands are never live at once (a 128-VGPR budget: 40 hold
+        // the A2 of this wave's units, 16 the gW3 accumulators)
+        float ad[KT];
 #pragma unroll
         for (int s = 0; s < KT; s++)
           ad[s] = s < F3 ? d3g[adb0 + 128 * j + (F3 - 1 - s)] : d3g[adb1 + 128 * j + 4 * (6 - s)];
@@ -322,47 +373,75 @@ __global__ __launch_bounds__(kL3RThreads, SRCNN_L3R_WAVES) void l3r_delta_kernel
         for (int t = 0; t < NT; t++)
 #pragma unroll
           for (int h = 0; h < 2; h++)
-            wv[t][h] = *reinterpret_cast<const f32x4*>(wds + wdo + 16 * t * kL3RWdS + 4 * h);
-#pragma unroll
-        for (int s = 0; s < 4; s++)
-#pragma unroll
-          for (int t3 = 0; t3 < TT; t3++) ag[s][t3] = d3g[agb[t3] + 128 * j + s];
-        f32x4 bg[NT];
-#pragma unroll
-        for (int t = 0; t < NT; t++) bg[t] = *reinterpret_cast<const f32x4*>(scw + sco_r + 16 * t * kL3RScS);
+            wv[t][h] = *reinterpret_cast<const f32x4*>(wds + wqo + 16 * t * kL3RWdS + 16 * h);
         f32x4 acc[NT];
 #pragma unroll
         for (int t = 0; t < NT; t++) acc[t] = mfma::zero4();
 #pragma unroll
         for (int s = 0; s < KT; s++)
 #pragma unroll
-          for (int t = 0; t < NT; t++) acc[t] = mfma::mma16(wv[t][s >> 2][s & 3], ad[s], acc[t]);
+          for (int t = 0; t < NT; t++)
+            if (!(SRCNN_L3R_DIAG & 4)) acc[t] = mfma::mma16(wv[t][s >> 2][s & 3], ad[s], acc[t]);
+        if (SRCNN_L3R_UNIT_FENCE) __builtin_amdgcn_sched_barrier(0);
+        // masked delta2; lane (lq, lg) holds quads lg (t = 0) and 4 + lg (t = 1)
+        // of pixel u0 + lq.  Two stores of WHOLE 128-B pixel rows: store A
+        // writes pixels u0 .. u0+7 and store B pixels u0+8 .. u0+15, 1 KB
+        // contiguous each (as held, each store covered half of 16 rows: the
+        // stores cost 43% of the kernel, SRCNN_L3R_DIAG=1 timing build)
+#pragma unroll
+        for (int t = 0; t < NT; t++)
+#pragma unroll
+          for (int i = 0; i < 4; i++) acc[t][i] = a2r[j][t][i] > 0.0f ? acc[t][i] : 0.0f;
+        if (!(SRCNN_L3R_DIAG & 1)) {
+          // through the scratch as [pixel][kL3RScS] rows: written as this
+          // lane's two quads, read back as whole rows
+#pragma unroll
+          for (int t = 0; t < NT; t++) *reinterpret_cast<f32x4*>(scw + srw + 16 * t) = acc[t];
+          const f32x4 sa = *reinterpret_cast<const f32x4*>(scw + srr);
+          const f32x4 sb = *reinterpret_cast<const f32x4*>(scw + srr + 8 * kL3RScS);
+          int l_ = lane;
+          asm volatile("" : "+v"(l_));  // (formed at the store, not held across the loop)
+          const unsigned o_ = (l_ & 7) * N2 + 4 * ((l_ >> 4) + 4 * ((l_ >> 3) & 1)) + 16 * nwaves * N2 * j;
+          if (u0 + (lq & 7) < npx2) st_d2(d2s + o_, sa);
+          if (u0 + 8 + (lq & 7) < npx2) st_d2(d2s + o_ + 8 * N2, sb);
+        }
+        if (SRCNN_L3R_UNIT_FENCE) __builtin_amdgcn_sched_barrier(0);
+        // gW3's B operand A2[u0 + 4lg + s][16t + lq] through the scratch
+#pragma unroll
+        for (int h = 0; h < 2; h++)
+#pragma unroll
+          for (int i = 0; i < 4; i++)
+            if (!(SRCNN_L3R_DIAG & 16)) scw[sco_w + (16 * h + i) * kL3RScS] = a2r[j][h][i];
+        float ag[4][TT];
+#pragma unroll
+        for (int s = 0; s < 4; s++)
+#pragma unroll
+          for (int t3 = 0; t3 < TT; t3++) ag[s][t3] = d3g[agb[t3] + 128 * j + s];
+        f32x4 bg[NT];
+#pragma unroll
+        for (int t = 0; t < NT; t++) bg[t] = *reinterpret_cast<const f32x4*>(scw + wqo + 16 * t * kL3RScS);
 #pragma unroll
         for (int s = 0; s < 4; s++)
 #pragma unroll
           for (int t3 = 0; t3 < TT; t3++)
 #pragma unroll
-            for (int t = 0; t < NT; t++) gacc[t3][t] = mfma::mma16(ag[s][t3], bg[t][s], gacc[t3][t]);
-        const int q = u0 + lq;
-        if (q < npx2) {
-          int o_ = a2lo + 16 * nwaves * N2 * j;
-          asm volatile("" : "+v"(o_));
-          float* dst = d2s + o_;
-#pragma unroll
-          for (int t = 0; t < NT; t++) {
-            f32x4 v;
-#pragma unroll
-            for (int i = 0; i < 4; i++) v[i] = a2r[j][t][i] > 0.0f ? acc[t][i] : 0.0f;
-            *reinterpret_cast<f32x4*>(dst + 16 * t) = v;
-          }
-        }
-        if (SRCNN_L3R_PF && has_next) SRCNN_L3R_LOAD(j, nsmp);
+            for (int t = 0; t < NT; t++)
+              if (!(SRCNN_L3R_DIAG & 8)) gacc[t3][t] = mfma::mma16(ag[s][t3], bg[t][s], gacc[t3][t]);
+        // the next sample's A2 into the registers this unit no longer needs
+        // (issued here rather than at the sample top: 0.158 vs 0.174 ms)
+        if (!(SRCNN_L3R_DIAG & 2)) SRCNN_L3R_LOAD(j, nsmp);
       }
     }
+    SRCNN_L3_TICK(3);
   }
 #undef SRCNN_L3R_LOAD
+#undef SRCNN_L3R_SWAP
 #undef SRCNN_L3R_T_PREFETCH
   SRCNN_CLOCK_END(g_clk, 1);
+#ifdef SRCNN_L3_TIMING
+  if (threadIdx.x == 0)
+    for (int k = 0; k < 4; k++) g_l3_timing[blockIdx.x][k] = tacc[k];
+#endif
 
   // ---- block reduction of the partial gradients, waves in order ----
   __syncthreads();

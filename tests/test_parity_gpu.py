@@ -388,8 +388,8 @@ def test_preload_every_net(S):
 @pytest.mark.parametrize("name,batch,size", [("default", 16, 33), ("wide", 3, 33), ("tiny", 5, 15),
                                              ("default", 2, 48), ("example", 7, 33),
                                              ("default", 3, 21), ("default", 600, 33),
-                                             # ragged against the grids: l3 (256 blocks, walks the
-                                             # batch from its end), l12 / d1 (512 blocks)
+                                             # ragged against the grids: l3r / l12 (512 blocks; l3r
+                                             # walks the batch from its end), d1c (1024)
                                              ("default", 257, 33), ("default", 513, 33),
                                              # the strong-scaling shard (512 tiles per rank) and its
                                              # neighbours; below 1024 samples d1c splits each
