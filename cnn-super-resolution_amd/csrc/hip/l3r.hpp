@@ -106,6 +106,9 @@ __device__ __forceinline__ void st_d2(float* p, f32x4 v) {
   else
     *reinterpret_cast<f32x4*>(p) = v;
 }
+#ifndef SRCNN_L3R_STAGGER
+#define SRCNN_L3R_STAGGER 0
+#endif
 #ifndef SRCNN_L3R_WAVES
 #define SRCNN_L3R_WAVES 4  // waves per SIMD: two 8-wave blocks per CU (128 VGPRs)
 #endif
@@ -263,6 +266,11 @@ __global__ __launch_bounds__(kL3RThreads, SRCNN_L3R_WAVES) void l3r_delta_kernel
     SRCNN_L3R_T_PREFETCH(s0);
   }
 
+  // stagger (A/B): the second half of the grid starts ~SRCNN_L3R_STAGGER x 8k
+  // cycles late, so that the blocks' memory-heavy delta2 phases do not all
+  // coincide
+  if (SRCNN_L3R_STAGGER > 0 && (int)blockIdx.x >= (int)gridDim.x / 2)
+    for (int k = 0; k < SRCNN_L3R_STAGGER; k++) __builtin_amdgcn_s_sleep(127);
 #ifdef SRCNN_L3_TIMING
   unsigned long long tacc[4] = {0, 0, 0, 0}, tlast = clock64();
 #endif
