@@ -96,19 +96,26 @@ static bool l3r_fits(int w2, int h2, int w3, int h3) {
 #ifndef SRCNN_L3R_UNIT_FENCE
 #define SRCNN_L3R_UNIT_FENCE 1
 #endif
-// D2 store cache policy (A/B): 0 default, 1 nontemporal
+// D2 store cache policy: 1 nontemporal (default), 0 plain (A/B)
 #ifndef SRCNN_L3R_D2NT
-#define SRCNN_L3R_D2NT 0
+#define SRCNN_L3R_D2NT 1
 #endif
+// A2 load cache policy: 1 nontemporal (default; A2 is read once), 0 plain.
+// Both nontemporal: l3 0.1578 / 0.1577 -> 0.1555 / 0.1552 ms (same-box A/B,
+// profiles/r04_ab_l3r/ab_l3r6)
+#ifndef SRCNN_L3R_A2NT
+#define SRCNN_L3R_A2NT 1
+#endif
+__device__ __forceinline__ f32x4 ld_a2(const float* p) {
+  if (SRCNN_L3R_A2NT) return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+  return *reinterpret_cast<const f32x4*>(p);
+}
 __device__ __forceinline__ void st_d2(float* p, f32x4 v) {
   if (SRCNN_L3R_D2NT)
     __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p));
   else
     *reinterpret_cast<f32x4*>(p) = v;
 }
-#ifndef SRCNN_L3R_STAGGER
-#define SRCNN_L3R_STAGGER 0
-#endif
 #ifndef SRCNN_L3R_WAVES
 #define SRCNN_L3R_WAVES 4  // waves per SIMD: two 8-wave blocks per CU (128 VGPRs)
 #endif
@@ -223,8 +230,8 @@ __global__ __launch_bounds__(kL3RThreads, SRCNN_L3R_WAVES) void l3r_delta_kernel
     const unsigned w_ = 16 * (wave + nwaves * (J)) * N2 + lo_;                          \
     const unsigned oa_ = pa_ < npx2 ? w_ : lo_; /* else pixel lq & 7 of the sample */   \
     const unsigned ob_ = pa_ + 8 < npx2 ? w_ + 8 * N2 : lo_;                            \
-    a2r[J][0] = *reinterpret_cast<const f32x4*>(b_ + oa_);                              \
-    a2r[J][1] = *reinterpret_cast<const f32x4*>(b_ + ob_);                              \
+    a2r[J][0] = ld_a2(b_ + oa_);                                                        \
+    a2r[J][1] = ld_a2(b_ + ob_);                                                        \
   } while (0)
   // loaded as whole 128-B pixel rows (store A / B of the D2 layout below);
   // at first use the lanes lq, lq ^ 8 swap one quad so that lane (lq, lg)
@@ -266,11 +273,6 @@ __global__ __launch_bounds__(kL3RThreads, SRCNN_L3R_WAVES) void l3r_delta_kernel
     SRCNN_L3R_T_PREFETCH(s0);
   }
 
-  // stagger (A/B): the second half of the grid starts ~SRCNN_L3R_STAGGER x 8k
-  // cycles late, so that the blocks' memory-heavy delta2 phases do not all
-  // coincide
-  if (SRCNN_L3R_STAGGER > 0 && (int)blockIdx.x >= (int)gridDim.x / 2)
-    for (int k = 0; k < SRCNN_L3R_STAGGER; k++) __builtin_amdgcn_s_sleep(127);
 #ifdef SRCNN_L3_TIMING
   unsigned long long tacc[4] = {0, 0, 0, 0}, tlast = clock64();
 #endif

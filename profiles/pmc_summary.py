@@ -20,6 +20,7 @@ from collections import defaultdict
 SHORT = [
     (r"l12_fwd_kernel", "l12_fwd_mfma"),
     (r"l3_delta_kernel", "l3_delta_fused"),
+    (r"l3r_delta_kernel", "l3_delta_fused"),
     (r"d1_grad12_kernel", "delta1_grad12_fused"),
     (r"d1c_grad12_kernel", "delta1_grad12_fused"),
     (r"slab_reduce_kernel", "slab_reduce"),
