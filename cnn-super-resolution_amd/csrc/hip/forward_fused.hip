@@ -83,6 +83,10 @@ __global__ __launch_bounds__(256, SRCNN_FWD_WAVES) void fwd_l123_kernel(
   constexpr int EHM = kFwdRhMax + F3 - 1;
   static_assert(K3 <= 32 && N2 <= 32 && N2 % 2 == 0 && K1 % 2 == 1, "Q tile shape");
   __shared__ float xs[kFwdXs];
+  // L2 bias as the accumulator's initial value: register r of half h is
+  // channel crow(r, h) (one 16x32 image, read as 4 broadcast 16-B loads)
+  // instead of one more MFMA (b2 x 1) per chunk; the same fp32 values
+  __shared__ __attribute__((aligned(16))) float b2i[2][16];
   // per-wave Q^T[tap][pixel + F3-1]: F3-1 zero columns either side, so a
   // window sum reads its F3 taps without bounds tests.  Row stride 52 floats
   // (5 x 52 = 4 mod 32): the window-sum items (dy, e) of one ds_read_b32 fall
@@ -136,6 +140,10 @@ __global__ __launch_bounds__(256, SRCNN_FWD_WAVES) void fwd_l123_kernel(
 #pragma unroll
     for (int s = 0; s < 16; s++) w2f[t][s] = li < N2 ? W2[(32 * t + crow(s, h)) * N2 + li] : 0.0f;
   const float b2a = (h == 0 && li < N2) ? B2[li] : 0.0f;
+  if (threadIdx.x < 32) {
+    const int c_ = crow(threadIdx.x & 15, threadIdx.x >> 4);
+    b2i[threadIdx.x >> 4][threadIdx.x & 15] = c_ < N2 ? B2[c_] : 0.0f;
+  }
   float w3f[16];
 #pragma unroll
   for (int s = 0; s < 16; s++) {
@@ -215,8 +223,17 @@ __global__ __launch_bounds__(256, SRCNN_FWD_WAVES) void fwd_l123_kernel(
         for (int r = 0; r < 16; r++)
           if (!(kFwdDiag & 4)) acc1[t][r] = fmaxf(acc1[t][r], 0.0f);
       // L2^T: A2^T[n][p] = B2[n] + sum_c W2[c][n] A1^T[c][p], then ReLU
-      f32x16 acc2 = zero16();
-      acc2 = mma(b2a, 1.0f, acc2);
+      f32x16 acc2;
+      if (SRCNN_B2_INIT) {
+      #pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const mfma::f32x4 v_ = *reinterpret_cast<const mfma::f32x4*>(&b2i[h][4 * q]);
+      #pragma unroll
+          for (int e = 0; e < 4; e++) acc2[4 * q + e] = v_[e];
+        }
+      } else {
+        acc2 = mma(b2a, 1.0f, zero16());
+      }
 #pragma unroll
       for (int t = 0; t < NT1; t++)
 #pragma unroll

@@ -115,6 +115,10 @@ __global__ __launch_bounds__(256, SRCNN_L12_WAVES) void l12_fwd_kernel(
   static_assert(N2 <= 32 && N2 % 8 == 0 && K1 % 2 == 1 && N1 % 32 == 0,
                 "transposed l12: one 32-row L2 tile, odd tap count");
   __shared__ float xs[kL12Tile];  // X tile at the fixed row stride kL12S (+ zero rows)
+  // L2 bias as the accumulator's initial value: register r of half h is
+  // channel crow(r, h) (one 16x32 image, read as 4 broadcast 16-B loads)
+  // instead of one more MFMA (b2 x 1) per chunk; the same fp32 values
+  __shared__ __attribute__((aligned(16))) float b2i[2][16];
 
   SRCNN_CLOCK_BEGIN();
   const int lane = mfma::lane_id(), wave = mfma::wave_id();
@@ -149,6 +153,10 @@ __global__ __launch_bounds__(256, SRCNN_L12_WAVES) void l12_fwd_kernel(
 #pragma unroll
     for (int s = 0; s < 16; s++) w2f[t][s] = li < N2 ? W2[(32 * t + crow(s, h)) * N2 + li] : 0.0f;
   const float b2a = (h == 0 && li < N2) ? B2[li] : 0.0f;
+  if (threadIdx.x < 32) {
+    const int c_ = crow(threadIdx.x & 15, threadIdx.x >> 4);
+    b2i[threadIdx.x >> 4][threadIdx.x & 15] = c_ < N2 ? B2[c_] : 0.0f;
+  }
 
   // The next sample's X tile is register-staged during the current sample
   // (its loads retire under the MFMAs instead of stalling both barriers);
@@ -258,8 +266,17 @@ __global__ __launch_bounds__(256, SRCNN_L12_WAVES) void l12_fwd_kernel(
       for (int t = 0; t < NT1; t++)
 #pragma unroll
         for (int r = 0; r < 16; r++) acc1[t][r] = fmaxf(acc1[t][r], 0.0f);
-      f32x16 acc2 = zero16();
-      acc2 = mma(b2a, 1.0f, acc2);
+      f32x16 acc2;
+      if (SRCNN_B2_INIT) {
+      #pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const f32x4 v_ = *reinterpret_cast<const f32x4*>(&b2i[h][4 * q]);
+      #pragma unroll
+          for (int e = 0; e < 4; e++) acc2[4 * q + e] = v_[e];
+        }
+      } else {
+        acc2 = mma(b2a, 1.0f, zero16());
+      }
 #pragma unroll
       for (int t = 0; t < NT1; t++)
 #pragma unroll
