@@ -103,6 +103,9 @@ constexpr int kL12Diag = SRCNN_L12_DIAG;
 #else
 constexpr int kL12Diag = 0;
 #endif
+#ifndef SRCNN_L3R_GRID
+#define SRCNN_L3R_GRID 512  // l3r grid cap: 256 CUs x 2 resident blocks
+#endif
 #ifndef SRCNN_L12_WAVES
 #define SRCNN_L12_WAVES 2  // minimum waves per SIMD (register budget 512 / this)
 #endif
@@ -970,7 +973,13 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
       l3r || (lds3 <= 160 * 1024 && w3 * h3 <= kL3MaxOut &&
               ((ow * oh + 15) / 16 + kL3Threads / 64 - 1) / (kL3Threads / 64) <= L3Lds<N2, F3>::kUnitsPerWave);
   const int g12 = grid_for_batch(batch, SRCNN_L12_GRID);
-  const int g3 = grid_for_batch(batch, l3r ? 512 : 256);
+  // l3r: up to 2 resident blocks per CU; between 256 and 1024 samples keep
+  // two samples per block, so the second sample's A2 loads run under the first
+  // one's delta2 phase (512 tiles: l3 0.0306 -> 0.0295 ms; at batch 4096 a
+  // 256-block grid is slower, 0.155 -> 0.167 ms; profiles/r04_ab_l3rgrid)
+  const int b3 = (int)batch;
+  const int g3 = l3r ? std::min(SRCNN_L3R_GRID, std::max(std::min(b3, 256), (b3 + 1) / 2))
+                     : grid_for_batch(batch, 256);
   const bool kD1c = SRCNN_D1C && N1 == 64 && N2 == 32 && F1 == 9 && d1c_fits(w, h);
   // d1c below kD1cGrid samples: each sample's chunks split into `parts`
   // ranges (work items), so the grid still fills every CU's 4 block slots
