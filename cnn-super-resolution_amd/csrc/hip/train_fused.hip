@@ -98,6 +98,8 @@ constexpr int kNtMask = SRCNN_NT;
 #endif
 constexpr int kL12PD = SRCNN_L12_PD;
 // diagnostics builds only (results invalid): 1 drop the A1 stores, 2 the A2 stores
+// (and with them the L2 MFMAs, dead code then), 4 the A2 stores behind a
+// runtime-false test (the L2 MFMAs stay)
 #ifdef SRCNN_L12_DIAG
 constexpr int kL12Diag = SRCNN_L12_DIAG;
 #else
@@ -106,6 +108,18 @@ constexpr int kL12Diag = 0;
 #ifndef SRCNN_L3R_GRID
 #define SRCNN_L3R_GRID 512  // l3r grid cap: 256 CUs x 2 resident blocks
 #endif
+// 1: A2 leaves l12 as whole 128-B pixel rows: at each chunk end the wave
+// regroups its A2 tile through a 4.6 KB LDS scratch into row order (one write
+// and one read per quad, a single LDS round trip per chunk), and the stores
+// inside the next chunk's MFMA stream write 1 KB contiguous each.  As held
+// (0), each store wrote 32 rows x 32 B; those stores cost 6% of l12
+// (SRCNN_L12_DIAG=4).  Same-box A/B (profiles/r04_ab_a2rows): l12 0.3068 ->
+// 0.3049 ms, l3 0.1559 -> 0.1547 ms, step 0.8668 -> 0.8641 ms at batch 4096;
+// the 512-tile shard unchanged (l12 +0.4 us)
+#ifndef SRCNN_L12_A2ROWS
+#define SRCNN_L12_A2ROWS 1
+#endif
+constexpr int kL12A2S = 36;  // A2 scratch row stride (floats)
 #ifndef SRCNN_L12_WAVES
 #define SRCNN_L12_WAVES 2  // minimum waves per SIMD (register budget 512 / this)
 #endif
@@ -118,6 +132,8 @@ __global__ __launch_bounds__(256, SRCNN_L12_WAVES) void l12_fwd_kernel(
   static_assert(N2 <= 32 && N2 % 8 == 0 && K1 % 2 == 1 && N1 % 32 == 0,
                 "transposed l12: one 32-row L2 tile, odd tap count");
   __shared__ float xs[kL12Tile];  // X tile at the fixed row stride kL12S (+ zero rows)
+  constexpr bool kA2Rows = SRCNN_L12_A2ROWS && N2 == 32;  // (a row = 8 quads)
+  __shared__ __attribute__((aligned(16))) float a2sc[kA2Rows ? 4 * 32 * kL12A2S : 4];
   // L2 bias as the accumulator's initial value: register r of half h is
   // channel crow(r, h) (one 16x32 image, read as 4 broadcast 16-B loads)
   // instead of one more MFMA (b2 x 1) per chunk; the same fp32 values
@@ -202,6 +218,7 @@ __global__ __launch_bounds__(256, SRCNN_L12_WAVES) void l12_fwd_kernel(
     bool pval = false;   // ... and this lane's pixel is inside the sample (A2)
     float* pa1p = A1;
     float* pa2p = A2;
+    int pc0 = 0;  // kA2Rows: the pending chunk's first pixel
     auto store_prev = [&](int k) {  // store k of the pending chunk (exec-masked)
       if (pok) {
         if (k < 4 * NT1 && !(kL12Diag & 1)) {
@@ -218,7 +235,17 @@ __global__ __launch_bounds__(256, SRCNN_L12_WAVES) void l12_fwd_kernel(
             *reinterpret_cast<float4*>(pa1p + 256 * k) =
                 make_float4(pa1[t][4 * q], pa1[t][4 * q + 1], pa1[t][4 * q + 2], pa1[t][4 * q + 3]);
           }
-        } else if (k >= 4 * NT1 && pval && !(kL12Diag & 2)) {
+        } else if (kA2Rows && k >= 4 * NT1 && !(kL12Diag & 2) && (!(kL12Diag & 4) || g.batch < 0)) {
+          // row store q: pixels 8q .. 8q + 7 of the chunk, lane L -> pixel
+          // 8q + L / 8, quad L % 8 (already relu'd, in pa2's quad q)
+          const int q = k - 4 * NT1;
+          if (pc0 + 8 * q + (lane >> 3) < npx) {
+            f32x4 v_;
+#pragma unroll
+            for (int e = 0; e < 4; e++) v_[e] = pa2[4 * q + e];
+            *reinterpret_cast<f32x4*>(pa2p + (8 * q + (lane >> 3)) * N2 + 4 * (lane & 7)) = v_;
+          }
+        } else if (!kA2Rows && k >= 4 * NT1 && pval && !(kL12Diag & 2) && (!(kL12Diag & 4) || g.batch < 0)) {
           const int q = k - 4 * NT1;
           *reinterpret_cast<float4*>(pa2p + 8 * q) =
               make_float4(fmaxf(pa2[4 * q], 0.0f), fmaxf(pa2[4 * q + 1], 0.0f),
@@ -288,11 +315,32 @@ __global__ __launch_bounds__(256, SRCNN_L12_WAVES) void l12_fwd_kernel(
       // channels 32t + 8q + 4h .. +3 of pixel pl
 #pragma unroll
       for (int t = 0; t < NT1; t++) pa1[t] = acc1[t];
-      pa2 = acc2;
+      if (kA2Rows) {
+        // A2 tile -> row order through this wave's scratch: register 4m + e
+        // of half h is channel 8m + 4h + e of pixel li (written relu'd); read
+        // back, quad q of this lane is pixel 8q + lane/8, channels 4 (lane%8)..
+        float* sc = a2sc + wave * 32 * kL12A2S;
+#pragma unroll
+        for (int m = 0; m < 4; m++) {
+          f32x4 v_;
+#pragma unroll
+          for (int e = 0; e < 4; e++) v_[e] = fmaxf(acc2[4 * m + e], 0.0f);
+          *reinterpret_cast<f32x4*>(sc + li * kL12A2S + 8 * m + 4 * h) = v_;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const f32x4 v_ = *reinterpret_cast<const f32x4*>(sc + (8 * q + (lane >> 3)) * kL12A2S + 4 * (lane & 7));
+#pragma unroll
+          for (int e = 0; e < 4; e++) pa2[4 * q + e] = v_[e];
+        }
+        pc0 = c * 32;
+      } else {
+        pa2 = acc2;
+      }
       pok = true;
       pval = pl < npx;
       pa1p = A1 + ((size_t)sample * nch + c) * (32 * N1) + 4 * lane;
-      pa2p = A2 + ((size_t)sample * npx + pc) * N2 + 4 * h;
+      pa2p = kA2Rows ? A2 + ((size_t)sample * npx + c * 32) * N2 : A2 + ((size_t)sample * npx + pc) * N2 + 4 * h;
     }
 #pragma unroll
     for (int k = 0; k < NST; k++) store_prev(k);
