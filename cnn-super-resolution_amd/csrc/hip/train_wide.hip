@@ -462,6 +462,9 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restri
 //   channel n, i.e. directly gW1's B operand (K = the 4 pixel slots); A = the
 //   X windows of 16-tap tiles (81 taps + the ones row: 6 tiles)
 // ---------------------------------------------------------------------------
+#ifndef SRCNN_D16_XCD
+#define SRCNN_D16_XCD 1  // d1g16: a sample's two channel halves on one XCD
+#endif
 #ifndef SRCNN_D16_MASK_AHEAD
 #define SRCNN_D16_MASK_AHEAD 3  // epilogue relu' loads run this many tiles ahead
 #endif
@@ -482,6 +485,15 @@ __global__ __launch_bounds__(256, 1) void d1g16_kernel(const float* __restrict__
   const int nt = wave & 1, mg = wave >> 1;
   const int buf_floats = g.img_w * g.img_h * kPS + kImgSlack;
   const int nitems = g.batch * NP;
+  // the NP parts of a sample (the same delta2 image) on one XCD: blocks go
+  // round-robin over the 8 XCDs, so parts of pair k run as blocks x, x + 8
+  int vb = blockIdx.x;
+#if SRCNN_D16_XCD
+  if (gridDim.x % (8 * NP) == 0) {
+    const int j = blockIdx.x / 8;
+    vb = (blockIdx.x % 8 + 8 * (j / NP)) * NP + j % NP;
+  }
+#endif
   float* const xsm = smem + 2 * buf_floats;  // 2 X tile buffers (item parity)
   int* const ptab = reinterpret_cast<int*>(xsm + 2 * kXBuf);
   // gW1 A operand: tap 16 tt + i16; tap NT1 - 1 (offset toffl) and gB1 by VALU
@@ -584,12 +596,12 @@ __global__ __launch_bounds__(256, 1) void d1g16_kernel(const float* __restrict__
   const int kdma = (g.img_w * g.img_h * 5 + 63) / 64;
   float* const buf0 = smem;
   float* const buf1 = smem + buf_floats;
-  if ((int)blockIdx.x < nitems)
-    for (int k = wave; k < kdma; k += 4) dma(blockIdx.x / NP, 0, buf0, k);
+  if (vb < nitems)
+    for (int k = wave; k < kdma; k += 4) dma(vb / NP, 0, buf0, k);
   wait_vm0();
   __syncthreads();
   int bsel = 0, ipar = 0;
-  for (int it = blockIdx.x; it < nitems; it += gridDim.x, ipar ^= 1) {
+  for (int it = vb; it < nitems; it += gridDim.x, ipar ^= 1) {
     const int s = it / NP, part = it - s * NP;
     xdma(it, ipar);  // lands before the first chunk barrier
     // B: N tile q of this wave is n16 = 4 part + 2 nt + q
@@ -744,10 +756,10 @@ __global__ __launch_bounds__(256, 1) void d1g16_kernel(const float* __restrict__
   }
   __syncthreads();
   if (mg == 0) {
-    float* o1 = slab1 + (size_t)(blockIdx.x / NP) * P1;
+    float* o1 = slab1 + (size_t)(vb / NP) * P1;
 #pragma unroll
     for (int q = 0; q < 2; q++) {
-      const int ch = (blockIdx.x % NP) * 64 + 32 * nt + 16 * q + i16;
+      const int ch = (vb % NP) * 64 + 32 * nt + 16 * q + i16;
 #pragma unroll
       for (int tt = 0; tt < TT; tt++)
 #pragma unroll
@@ -1166,6 +1178,12 @@ __global__ __launch_bounds__(512, 1) void wl3l_kernel(const float* __restrict__ 
 // delta2 rows (64 channels, 80-float pixels) are DMA'd into LDS, double
 // buffered across bands; the compute loop only reads LDS.
 // ---------------------------------------------------------------------------
+#ifndef SRCNN_WG2_XCD
+#define SRCNN_WG2_XCD 1  // a sample group's channel-quarter blocks on one XCD
+#endif
+#ifndef SRCNN_WG2_HALO
+#define SRCNN_WG2_HALO 1  // band halo rows copied LDS -> LDS from the previous band
+#endif
 constexpr int kGAS = 48;      // LDS floats per A1 pixel (32 channels + pad)
 constexpr int kGDS = 80;      // LDS floats per delta2 pixel (64 channels + pad)
 constexpr int kBandPx = 64;   // output pixels per band (16 quads)
@@ -1192,7 +1210,17 @@ __global__ __launch_bounds__(512, 1) void wgrad2_kernel(const float* __restrict_
   extern __shared__ float smem[];
   const int lane = lane_id(), wave = wave_id(), i = lane & 15, gq = lane >> 4;
   const int ct = wave & 1, nt = wave >> 1;
-  const int cq = blockIdx.x % NCQ, grp = blockIdx.x / NCQ;
+  int cq = blockIdx.x % NCQ, grp = blockIdx.x / NCQ;
+#if SRCNN_WG2_XCD
+  if (gridDim.x % (8 * NCQ) == 0) {
+    // blocks go round-robin over the 8 XCDs: blocks x, x + 8, ... share an
+    // XCD, so a group's NCQ channel quarters are put there and read each
+    // delta2 band from that XCD's L2 instead of NCQ times from HBM
+    const int j = blockIdx.x / 8;
+    cq = j % NCQ;
+    grp = blockIdx.x % 8 + 8 * (j / NCQ);
+  }
+#endif
   const bool gbw = cq == 0 && ct == 0;
   f32x4 acc[FF];
 #pragma unroll
@@ -1214,7 +1242,7 @@ __global__ __launch_bounds__(512, 1) void wgrad2_kernel(const float* __restrict_
   // units = (sample, band) of this group
   const int nsamp = g.batch > grp ? (g.batch - grp + g.groups - 1) / g.groups : 0;
   const int nunits = nsamp * g.nbands;
-  auto stage = [&](int u, float* buf) {
+  auto stage = [&](int u, float* buf, const float* prev) {
     const int s = grp + (u / g.nbands) * g.groups, b = u % g.nbands, by = b / g.nbx;
     const int y0 = by * g.rows, rb = min(g.rows, g.h2 - y0);
     const int x0 = (b - by * g.nbx) * g.cols, cb = min(g.cols, g.w2 - x0);
@@ -1224,8 +1252,20 @@ __global__ __launch_bounds__(512, 1) void wgrad2_kernel(const float* __restrict_
     const float* asrc = A1 + ((size_t)s * g.h1 * g.w1 + (size_t)y0 * g.w1 + x0) * CIN + 32 * cq;
     const int dslots = (kBandPx + 4) * 20;
     const float* dsrc = D2 + ((size_t)s * g.h2 * g.w2 + (size_t)y0 * g.w2 + x0) * COUT;
+    int k0 = 0;  // first 64-slot DMA group of the A1 image that comes from HBM
+#if SRCNN_WG2_HALO
+    if (g.nbx == 1 && b > 0 && prev) {
+      // the band's first F - 1 A1 rows are the previous band's last F - 1 rows
+      // (that band is full, rows = g.rows), already in LDS: copied LDS -> LDS in
+      // whole 64-slot groups, the rest DMA'd, so each A1 row leaves HBM once
+      k0 = (F - 1) * aw * 12 / 64;
+      const float4* src = reinterpret_cast<const float4*>(prev + g.rows * aw * kGAS);
+      float4* dst = reinterpret_cast<float4*>(buf);
+      for (int e = threadIdx.x; e < k0 * 64; e += 512) dst[e] = src[e];
+    }
+#endif
     if (g.nbx == 1) {  // full-width bands: the band's rows are contiguous in HBM
-      for (int k = wave; k * 64 < aslots; k += 8) {
+      for (int k = k0 + wave; k * 64 < aslots; k += 8) {
         const int slot = k * 64 + lane, pix = slot / 12, q = slot - 12 * pix;
         const bool ok = q < 8 && slot < aslots;
         dma16(ok ? asrc + (size_t)pix * CIN + 4 * q : g_zero_src, buf + k * 256);
@@ -1252,12 +1292,12 @@ __global__ __launch_bounds__(512, 1) void wgrad2_kernel(const float* __restrict_
     }
   };
   int bsel = 0;
-  if (nunits > 0) stage(0, smem);
+  if (nunits > 0) stage(0, smem, nullptr);
   for (int u = 0; u < nunits; u++) {
     wait_vm0();
     __syncthreads();  // unit u landed; everyone is done with the other buffer
     const float* cur = smem + (bsel ? kGBuf : 0);
-    if (u + 1 < nunits) stage(u + 1, smem + (bsel ? 0 : kGBuf));
+    if (u + 1 < nunits) stage(u + 1, smem + (bsel ? 0 : kGBuf), cur);
     // k-step kq's operands (delta2 value + the F*F A1 taps) are read one
     // k-step ahead into two named register sets, pinned by sched_barriers:
     // left alone, the scheduler reads two taps at a time right before their
