@@ -68,6 +68,22 @@ __device__ __forceinline__ void dma16(const float* src, float* lds_dst) {
                : "s"(__builtin_amdgcn_readfirstlane(lds_addr(lds_dst))), "v"(src)
                : "m0");
 }
+// the same DMA with the nontemporal hint, for input images each block reads
+// once (conv_mfma, d1g16), so they pass through L2 without evicting the
+// W2 operand images every block re-reads
+#ifndef SRCNN_WIDE_DMA_NT
+#define SRCNN_WIDE_DMA_NT 0
+#endif
+__device__ __forceinline__ void dma16_stream(const float* src, float* lds_dst) {
+#if SRCNN_WIDE_DMA_NT
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt"
+               :
+               : "s"(__builtin_amdgcn_readfirstlane(lds_addr(lds_dst))), "v"(src)
+               : "m0");
+#else
+  dma16(src, lds_dst);
+#endif
+}
 __device__ __forceinline__ void dma4(const float* src, float* lds_dst) {
   asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dword %1, off"
                :
@@ -304,7 +320,7 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restri
                     ((unsigned)x < (unsigned)g.in_w);
     const float* base = in + ((size_t)wn.s * g.in_h * g.in_w) * CIN + c * kCC;
     const float* src = ok ? base + (y * g.in_w + x) * CIN + 4 * q : g_zero_src;
-    dma16(src, buf + k * 256);
+    dma16_stream(src, buf + k * 256);
   };
   auto kdma_of = [](const CWin& wn) { return (wn.iw * wn.ih * 5 + 63) / 64; };
   float* const buf0 = smem;
@@ -591,7 +607,7 @@ __global__ __launch_bounds__(256, 1) void d1g16_kernel(const float* __restrict__
                     ((unsigned)x < (unsigned)g.in_w);
     const float* base = in + ((size_t)s * g.in_h * g.in_w) * CIN + c * kCC;
     const float* src = ok ? base + (y * g.in_w + x) * CIN + 4 * q : g_zero_src;
-    dma16(src, buf + k * 256);
+    dma16_stream(src, buf + k * 256);
   };
   const int kdma = (g.img_w * g.img_h * 5 + 63) / 64;
   float* const buf0 = smem;
