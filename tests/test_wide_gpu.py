@@ -79,8 +79,11 @@ def split_ws(ws, w, h, batch):
     return out
 
 
+# batch 8: the smallest batch whose d1g16 (16 blocks) and wgrad2 (32 blocks)
+# grids take the XCD-aware block mapping; the other small batches run the
+# plain mapping, batch 64 / 300 / 4096 (below) the mapped one at full grids
 @pytest.mark.parametrize("w,h,batch", [(33, 33, 1), (33, 33, 6), (29, 29, 3), (33, 27, 2),
-                                       (25, 31, 3)])
+                                       (25, 31, 3), (33, 33, 8)])
 def test_wide_step_stages_vs_oracle(S, w, h, batch):
     X, T, params, g0, got, err, ws, stats = run_step(S, w, h, batch, seed=7 + w + h + batch)
     assert "wide_l2_fwd" in stats and "wide_grad2" in stats, stats.keys()
