@@ -569,45 +569,96 @@ def spawn_ranks(n, argv):
     return subprocess.call(cmd, env=env)
 
 
+class CudaDevice:
+    """This rank's GPU as the bench uses it: the torch device (memory only),
+    the HIP stream the headline runs on (graph capture needs a created
+    stream) and a device-wide sync.  The CPU tests inject a stand-in."""
+
+    def __init__(self, index):
+        torch.cuda.set_device(index)
+        self.dev = torch.device("cuda", index)
+        self.hstream = torch.cuda.Stream(device=self.dev)
+        self.stream = self.hstream.cuda_stream
+
+    def sync(self):
+        torch.cuda.synchronize()
+
+    def on_stream(self):
+        """torch work (a torch.distributed collective) ordered on the headline stream"""
+        return torch.cuda.stream(self.hstream)
+
+
+def reduce_int(v, op, world, backend, dev):
+    """MIN / MAX of an int over the process group (every rank gets it)."""
+    if world <= 1:
+        return int(v)
+    t = torch.tensor([int(v)], dtype=torch.int64, device=dev if backend == "nccl" else "cpu")
+    dist.all_reduce(t, op=op)
+    return int(t.item())
+
+
 def agree_all(flag, world, backend, dev):
     """True on every rank iff `flag` is true on every rank (MIN over the
-    process group), so that all ranks take the same branch before a
-    collective-carrying HIP graph is replayed."""
-    if world <= 1:
-        return bool(flag)
-    t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=dev if backend == "nccl" else "cpu")
-    dist.all_reduce(t, op=dist.ReduceOp.MIN)
-    return bool(t.item())
+    process group), so that all ranks take the same branch."""
+    return bool(reduce_int(1 if flag else 0, dist.ReduceOp.MIN if world > 1 else None, world, backend, dev))
 
 
-def timed_region(step, steps, warmup, world, every, stream, S, graph_mode, backend, dev):
+def settle(step, settle_ms, sync, world, backend, dev, probe=3):
+    """Untimed steps of the timed workload itself, run right before its W
+    warmup steps, until ~settle_ms of it has executed: the chip's clock keeps
+    moving for ~20 ms after a change of workload (rocprofv3 trace of the
+    driver's command, profiles/r05_clock: the headline kernels 5-8% slow over
+    steps 3-8 after the 4K frames, steady from step ~20), so a short timed
+    region (--steps 20 --warmup 5) would otherwise time that transient.  The
+    step count is agreed over the ranks (MAX): the steps carry the gradient
+    all-reduce, so every rank must run the same number.  Returns the count."""
+    if settle_ms <= 0:
+        return 0
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(probe):
+        step()
+    sync()
+    per_ms = max((time.perf_counter() - t0) / probe * 1e3, 1e-3)
+    n = reduce_int(int(settle_ms / per_ms + 0.999), dist.ReduceOp.MAX if world > 1 else None, world,
+                   backend, dev)
+    for _ in range(n):
+        step()
+    sync()
+    return probe + n
+
+
+def timed_region(step, steps, warmup, world, every, stream, S, graph_mode, backend, dev, sync):
     """W untimed warmup steps, then K timed steps bracketed by a barrier and a
     device sync on both sides; returns (elapsed max over ranks, profiled
     steps, whether a HIP graph was replayed).  Per-kernel hipEvents on every
-    `every`-th step (or on as many extra steps after a graph replay)."""
+    `every`-th step (or on as many extra steps after a graph replay).
+    graph_mode (one rank only: a step is then one srcnn_train_step, no
+    collective): the timed steps replay one captured step."""
     for _ in range(warmup):
         step()
-    torch.cuda.synchronize()
+    sync()
     graph = None
     if graph_mode:
         ok = True
         try:
             graph = S.Graph(step, stream)
-            graph.launch()  # one untimed replay
-            torch.cuda.synchronize()
-        except S.SrcnnError as e:  # e.g. a collective that cannot be captured
+        except S.SrcnnError as e:
             print("[bench] HIP graph capture failed (%s)" % e, file=sys.stderr)
             ok = False
-        # every rank must take the same branch: a graph replay carries the
-        # all-reduce, so mixed graph / direct ranks would mismatch collectives
+        # agree before anything is replayed (advisor r04): no rank may run a
+        # captured step unless every rank captured one
         if not agree_all(ok, world, backend, dev):
             if graph is not None:
                 graph.close()
             graph = None
             print("[bench] HIP graph not used on every rank; timing direct calls", file=sys.stderr)
+        if graph is not None:
+            graph.launch()  # one untimed replay
+            sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     S.profile_reset()
     n_prof = 0
     t0 = time.perf_counter()
@@ -620,7 +671,7 @@ def timed_region(step, steps, warmup, world, every, stream, S, graph_mode, backe
             n_prof += on
             S.profile_enable(on)
             step()
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -630,7 +681,7 @@ def timed_region(step, steps, warmup, world, every, stream, S, graph_mode, backe
         S.profile_enable(True)
         for _ in range(n_prof):
             step()
-        torch.cuda.synchronize()
+        sync()
         S.profile_enable(False)
         graph.close()
     if world > 1:
@@ -640,7 +691,7 @@ def timed_region(step, steps, warmup, world, every, stream, S, graph_mode, backe
     return elapsed, n_prof, graph is not None
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1,
                     help="GPUs of this node, one rank each; without torch.distributed.run the "
@@ -650,6 +701,9 @@ def main():
     # launches, flat over the next 275), so the default run warms up past it
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--settle-ms", type=float, default=50.0,
+                    help="untimed steps of the timed workload (~this many ms of them) before its "
+                         "warmup, so the timed steps start at the steady clock (see settle())")
     ap.add_argument("--batch", type=int, default=4096,
                     help="tiles per GPU per step (weak scaling, the default line)")
     ap.add_argument("--global-batch", type=int, default=None,
@@ -667,13 +721,14 @@ def main():
     # default; torch.distributed then only ships the RCCL id and runs the
     # barriers / max-time reduction (gloo).  --comm torch uses dist.all_reduce.
     ap.add_argument("--comm", choices=["srcnn", "torch"], default="srcnn")
-    # --graph on: the timed steps replay one HIP graph of the step
-    # (srcnn_graph_*): the same kernels and collective without a host launch
-    # per kernel; the ranks agree on its use (agree_all) before any replay.
-    # Default off: at N = 1 it measured the same (0.8975 vs 0.894 ms, same
-    # box), the direct calls enqueue well ahead of the GPU even at 512 tiles
-    # per rank, and a captured multi-rank RCCL collective has not been
-    # replayed on more than one GPU yet
+    # N > 1: one step = srcnn_train_fwd_bwd_lazy (the previous step's update
+    # inside its first kernel) + the all-reduce; --dp-step separate keeps the
+    # update as its own launch after the all-reduce (A/B)
+    ap.add_argument("--dp-step", choices=["lazy", "separate"], default="lazy")
+    # --graph on (one GPU): the timed steps replay one HIP graph of the step
+    # (srcnn_graph_*).  Default off: it measured the same (0.8975 vs 0.894 ms,
+    # same box); the direct calls enqueue well ahead of the GPU.  N > 1 steps
+    # ping-pong parameter buffers on the host, so they are always direct calls
     ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto")
     ap.add_argument("--no-strong", action="store_true",
                     help="N > 1: skip the strong-scaling sub-record (global batch 4096)")
@@ -682,27 +737,56 @@ def main():
     # rehearsal of the N>1 path on a single-GPU box (NOT a measurement):
     # every rank on one device, gradients all-reduced over gloo
     ap.add_argument("--all-ranks-on-device", type=int, default=None)
-    args = ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def main(argv=None, S=None, device=None):
+    """Entry point (argv = sys.argv[1:] by default).  `S` (the srcnn_amd
+    binding) and `device` (a CudaDevice-like object: dev, stream, sync,
+    on_stream) are injectable so that the CPU tests can drive the multi-rank
+    path with a stand-in library; the bench itself uses neither argument."""
+    if argv is None:
+        argv = sys.argv[1:]
+    args = parse_args(argv)
     mode, world = launch_plan(args.gpus, os.environ)
     if mode == "spawn":
-        sys.exit(spawn_ranks(world, sys.argv[1:]))
-
-    import srcnn_amd as S
+        sys.exit(spawn_ranks(world, argv))
+    if S is None:
+        import srcnn_amd as S
     from srcnn_amd import parallel
-
     rank, world, local = parallel.env_world()
+    try:
+        run(args, S, parallel, rank, world, local, device)
+    except BaseException as e:
+        if world <= 1:
+            raise
+        # one rank failed: leave at once, so no peer stays blocked in a
+        # collective of this rank's -- gloo peers see the closed connections
+        # and fail (then exit here too), torch.distributed.run stops the rest,
+        # and the group's timeout bounds the remaining cases.  os._exit skips
+        # the teardown (RCCL communicator, process group) that could itself
+        # block on the dead peers.
+        code = e.code if isinstance(e, SystemExit) and isinstance(e.code, int) and e.code else 1
+        if not (isinstance(e, SystemExit) and e.code is None):
+            import traceback
+            print("[bench rank %d/%d] failed: %s" % (rank, world, e), file=sys.stderr)
+            traceback.print_exc()
+        sys.stderr.flush()
+        sys.stdout.flush()
+        os._exit(code)
+
+
+def run(args, S, parallel, rank, world, local, device=None):
     dev_index = local if world > 1 else 0
     if args.all_ranks_on_device is not None:
         dev_index = args.all_ranks_on_device
     backend = args.dist_backend or ("gloo" if args.comm == "srcnn" else "nccl")
-    torch.cuda.set_device(dev_index)
-    parallel.init(backend, torch.device("cuda", dev_index))
+    D = device if device is not None else CudaDevice(dev_index)
+    parallel.init(backend, D.dev if D.dev.type == "cuda" else None)
     S.set_path(0 if args.path == "auto" else 1)
-    dev = torch.device("cuda", torch.cuda.current_device())
-    # the headline runs on a stream of its own (graph capture needs a created
-    # stream); the inputs are made on torch's stream, synchronised before use
-    hstream = torch.cuda.Stream(device=dev)
-    stream = hstream.cuda_stream
+    dev = D.dev
+    stream = D.stream
+    sync = D.sync
 
     net_t = DEFAULT_NET
     net = S.Net(*net_t)
@@ -730,6 +814,7 @@ def main():
     ws_bytes = S.train_workspace_bytes(net, w, h, Bmax)
     ws = torch.empty(ws_bytes // 4 + 64, dtype=torch.float32, device=dev)
     lr = [1e-4, 1e-4, 1e-5]
+    mu, wd = 0.9, 1e-3
 
     comm = None
     rccl_ranks = None
@@ -742,15 +827,41 @@ def main():
                              % (c_rank, rccl_ranks, rank, world))
     elif world > 1 and backend == "nccl":
         rccl_ranks = dist.get_world_size()
+    allreduce = comm
+    if world > 1 and comm is None:
+        def allreduce(g):  # dist.all_reduce ordered on the stream the kernels run on
+            with D.on_stream():
+                dist.all_reduce(g, op=dist.ReduceOp.SUM)
+
+    lazy = world > 1 and args.dp_step == "lazy"
+    # the lazy step ping-pongs the parameters / momentum; `bufs` holds the
+    # current pair first
+    bufs = {"p": params, "m": mom, "p2": torch.empty_like(params) if lazy else None,
+            "m2": torch.empty_like(mom) if lazy else None}
 
     def dp_step(batch, global_batch):
         """One rank's shard -> grads; one all-reduce; the same update on every
         rank (srcnn_amd/parallel.py)."""
+        if lazy:
+            return parallel.LazyDataParallelStep(
+                bufs["p"], bufs["p2"], bufs["m"], bufs["m2"], grads,
+                lambda pi, po, mi, mo, g, pend: S.train_fwd_bwd_lazy(
+                    net, Xd, Td, w, h, batch, pi, po, mi, mo, g, mu, wd, lr, pend, None, ws, ws_bytes,
+                    stream),
+                lambda p, m, g, nb: S.update_all(net, p, g, m, mu, wd, lr, nb, stream),
+                global_batch, allreduce=allreduce)
         return parallel.DataParallelStep(
             grads,
-            lambda g: S.train_fwd_bwd(net, Xd, Td, w, h, batch, params, g, None, ws, ws_bytes, stream),
-            lambda nb: S.update_all(net, params, grads, mom, 0.9, 1e-3, lr, nb, stream),
-            global_batch, allreduce=comm)
+            lambda g: S.train_fwd_bwd(net, Xd, Td, w, h, batch, bufs["p"], g, None, ws, ws_bytes, stream),
+            lambda nb: S.update_all(net, bufs["p"], grads, bufs["m"], mu, wd, lr, nb, stream),
+            global_batch, allreduce=allreduce)
+
+    def finish(step):
+        """apply a lazy step's owed update; its current buffers become bufs'"""
+        if isinstance(step, parallel.LazyDataParallelStep):
+            p, m = step.finish()
+            if p is not bufs["p"]:
+                bufs["p"], bufs["p2"], bufs["m"], bufs["m2"] = p, bufs["p"], m, bufs["m"]
 
     step = dp_step(B, global_tiles)
     if world == 1 and not os.environ.get("SRCNN_BENCH_SEPARATE_UPDATE"):
@@ -758,7 +869,7 @@ def main():
         # fused path the update runs inside the gradient reduction).
         # SRCNN_BENCH_SEPARATE_UPDATE=1: fwd_bwd + update_all (A/B)
         def step():
-            S.train_step(net, Xd, Td, w, h, B, params, grads, mom, 0.9, 1e-3, lr, global_tiles,
+            S.train_step(net, Xd, Td, w, h, B, params, grads, mom, mu, wd, lr, global_tiles,
                          None, ws, ws_bytes, stream)
 
     # The single-GPU side lines (the wide net, one 256x256 tile, 4K inference)
@@ -767,27 +878,28 @@ def main():
     # wide net's full-power load the GPU stalls the next launch for 8-24 ms
     # (a power-state transition; a 0.2 s idle pause avoids it), and a step
     # launched on an idle GPU runs through a ~25 ms clock ramp.  So: wide net,
-    # a pause, then the two inference lines, then the headline's W warmup +
-    # K timed steps, which thereby run at the steady clock of sustained load.
-    # With N > 1 every rank runs the same sequence on its own GPU, so that each
-    # N's headline starts from the same power state (a rank that skipped it
-    # would time its warmup through the idle clock ramp and the scaling curve
-    # would charge that to N); only N = 1 reports these lines.
+    # a pause, then the two inference lines, then settle() steps of the
+    # headline's own workload, then its W warmup + K timed steps, which
+    # thereby run at the steady clock of sustained load.  With N > 1 every
+    # rank runs the same sequence on its own GPU, so that each N's headline
+    # starts from the same power state (a rank that skipped it would time its
+    # warmup through the idle clock ramp and the scaling curve would charge
+    # that to N); only N = 1 reports these lines.
     S.preload(net)
     side = {}
     if not args.no_wide:
         side["wide"] = wide_training(S)
-        torch.cuda.synchronize()
+        sync()
         time.sleep(0.5)
     if not args.no_forward:
         side["forward_tile_256"] = forward_tile_256(S, net_t)
         side["forward"] = forward_4k(S, net_t)
     if world > 1:
         side = {}
-    torch.cuda.synchronize()
+    sync()
     _mark("side legs done")
 
-    graph_mode = args.graph == "on" and (world == 1 or comm is not None)
+    graph_mode = args.graph == "on" and world == 1
     every = max(1, min(args.profile_every, args.steps))
     # Per-kernel durations come from hipEvent pairs recorded around the
     # launches of every `every`-th timed step (steps every-1, 2*every-1, ...:
@@ -795,31 +907,35 @@ def main():
     # every launch cost 2.5% of the step even as fence-free timing events
     # (1.011 vs 0.986 ms, same box), so the sampled steps carry the
     # instrumentation and the others run bare.
+    n_settle = settle(step, args.settle_ms, sync, world, backend, dev)
     elapsed, n_prof, used_graph = timed_region(step, args.steps, args.warmup, world, every, stream, S,
-                                               graph_mode, backend, dev)
+                                               graph_mode, backend, dev, sync)
     _mark("headline timed steps done")
     kernel_path = S.last_path()
     stats = S.profile_stats()
+    finish(step)
 
     # N > 1: the strong-scaling step in the same run (global batch 4096
     # sharded over the ranks: 512 tiles per rank at N = 8), timed the same way
     strong_rec = None
     if world > 1 and not strong and not args.no_strong:
         sstep = dp_step(Bs, STRONG_GLOBAL_BATCH)
+        s_settle = settle(sstep, args.settle_ms, sync, world, backend, dev)
         s_el, s_prof, s_graph = timed_region(sstep, args.steps, args.warmup, world, every, stream, S,
-                                             graph_mode, backend, dev)
+                                             graph_mode, backend, dev, sync)
         s_stats = S.profile_stats()
+        finish(sstep)
         s_ms = s_el / args.steps * 1e3
         strong_rec = {
             "scaling": "strong", "global_batch": STRONG_GLOBAL_BATCH, "batch_per_gpu": Bs,
             "value": round(STRONG_GLOBAL_BATCH * args.steps / s_el, 1), "unit": "tiles/s",
             "ms_per_step": round(s_ms, 4), "steps": args.steps, "warmup": args.warmup,
-            "hip_graph": s_graph,
+            "settle_steps": s_settle, "hip_graph": s_graph,
             "kernels": {k: {"launches_per_step": c / max(s_prof, 1), "ms_per_step": round(t / max(s_prof, 1), 4)}
                         for k, (c, t) in s_stats.items()},
             "note": "rank 0's per-kernel split; value = 4096 tiles x steps / max-over-ranks time"}
         _mark("strong timed steps done")
-    assert np.isfinite(params.cpu().numpy()).all(), "non-finite parameters after training"
+    assert np.isfinite(bufs["p"].cpu().numpy()).all(), "non-finite parameters after training"
     fwd_sharded = None
     if world > 1 and not args.no_forward:
         def reduce_max(v):
@@ -862,6 +978,14 @@ def main():
             strong_rec = {"scaling": "strong", "global_batch": B, "batch_per_gpu": B,
                           "value": round(value, 1), "unit": "tiles/s", "ms_per_step": round(ms_step, 4),
                           "note": "N = 1: the headline step (global batch 4096 on one GPU)"}
+        if world == 1:
+            step_call = ("srcnn_train_fwd_bwd + srcnn_update_all" if os.environ.get("SRCNN_BENCH_SEPARATE_UPDATE")
+                         else "srcnn_train_step (SGD update inside the gradient reduction)")
+        elif lazy:
+            step_call = ("srcnn_train_fwd_bwd_lazy (the previous step's SGD update inside its first "
+                         "kernel) + the gradient all-reduce")
+        else:
+            step_call = "srcnn_train_fwd_bwd + the gradient all-reduce + srcnn_update_all"
         out = {
             "metric": metric,
             "value": round(value, 1),
@@ -879,9 +1003,8 @@ def main():
                        "tile": "33x33", "parallelism": "dp%d" % world,
                        "kernel_path": kernel_path,
                        "hip_graph": used_graph,
-                       "step_call": ("srcnn_train_fwd_bwd + srcnn_update_all" if world > 1 or
-                                     os.environ.get("SRCNN_BENCH_SEPARATE_UPDATE") else
-                                     "srcnn_train_step (SGD update inside the gradient reduction)"),
+                       "settle_steps": n_settle,
+                       "step_call": step_call,
                        "grad_allreduce": (("srcnn_allreduce_grads (RCCL)" if comm else
                                            "torch.distributed all_reduce (%s)" % backend)
                                           if world > 1 else None),

@@ -315,11 +315,12 @@ static TrainWs train_ws(const NetDims& d, uint32_t batch, void* ws) {
 static int train_impl(const srcnn_net* net, const float* X, const float* T, uint32_t w,
                       uint32_t h, uint32_t batch, const float* params, float* grads,
                       float* sq_err, void* ws, size_t ws_bytes, srcnn_stream_t stream,
-                      const srcnn::fused::SlabUpdate* up, bool* updated) {
+                      const srcnn::fused::SlabUpdate* up, bool* updated,
+                      const srcnn::fused::LazyUpdate* lz = nullptr) {
   NetDims d;
   if (int rc = net_dims(net, w, h, &d)) return rc;
   if (batch == 0) return SRCNN_OK;
-  SRCNN_REQUIRE(X && T && params && grads && ws, "train_fwd_bwd: null buffer");
+  SRCNN_REQUIRE(X && T && grads && ws && (params || (lz && lz->batch > 0.0f)), "train_fwd_bwd: null buffer");
   const size_t need = srcnn_train_workspace_bytes(net, w, h, batch);
   if (ws_bytes < need)
     return fail(SRCNN_ERR_WORKSPACE, "train_fwd_bwd: workspace %zu B < %zu B", ws_bytes, need);
@@ -329,17 +330,29 @@ static int train_impl(const srcnn_net* net, const float* X, const float* T, uint
   float *A1 = L.A1, *D1 = L.D1, *A2 = L.A2, *D2 = L.D2, *A3 = L.A3, *D3 = L.D3;
   void* gws = L.gws;
   const size_t gws_bytes = ws_bytes - (size_t)(static_cast<char*>(gws) - static_cast<char*>(ws));
-  const float *W1 = params + off[0], *B1 = params + off[1], *W2 = params + off[2],
-              *B2 = params + off[3], *W3 = params + off[4], *B3 = params + off[5];
-  float *gW1 = grads + off[0], *gB1 = grads + off[1], *gW2 = grads + off[2],
-        *gB2 = grads + off[3], *gW3 = grads + off[4], *gB3 = grads + off[5];
   int rc;
   if (fast_enabled()) {
     rc = srcnn::fused::train_fwd_bwd(net, X, T, w, h, batch, params, grads, sq_err, A1, A2, D2, A3,
                                      D3, static_cast<float*>(gws), gws_bytes,
-                                     srcnn::as_stream(stream), false, nullptr, up);
+                                     srcnn::as_stream(stream), false, nullptr, up, lz);
     if (rc == 2 && updated) *updated = true;
     if (rc != 0) return rc < 0 ? rc : tag("fused", SRCNN_OK);
+  }
+  if (lz) {
+    // srcnn_train_fwd_bwd_lazy off the fused path: the pending update out of
+    // place and the gradients zeroed in one launch, then the accumulating step
+    if (lz->batch > 0.0f) {
+      if ((rc = srcnn::lazy_update(*lz, srcnn::as_stream(stream)))) return rc;
+      params = lz->Po;
+    } else if ((rc = srcnn::fill(grads, 0.0f, off[5] + 1, srcnn::as_stream(stream)))) {
+      return rc;
+    }
+  }
+  const float *W1 = params + off[0], *B1 = params + off[1], *W2 = params + off[2],
+              *B2 = params + off[3], *W3 = params + off[4], *B3 = params + off[5];
+  float *gW1 = grads + off[0], *gB1 = grads + off[1], *gW2 = grads + off[2],
+        *gB2 = grads + off[3], *gW3 = grads + off[4], *gB3 = grads + off[5];
+  if (fast_enabled()) {
     rc = srcnn::wide::train_fwd_bwd(net, X, T, w, h, batch, params, grads, sq_err, A1, D1, A2, D2,
                                     A3, static_cast<float*>(gws), gws_bytes,
                                     srcnn::as_stream(stream), false, nullptr, up);
@@ -406,6 +419,45 @@ int srcnn_train_step(const srcnn_net* net, const float* X, const float* T, uint3
     return rc;
   if (updated) return SRCNN_OK;
   return srcnn_update_all(net, params, grads, momentum_bufs, momentum, wd, lr, update_batch, stream);
+}
+
+int srcnn_train_fwd_bwd_lazy(const srcnn_net* net, const float* X, const float* T, uint32_t w,
+                             uint32_t h, uint32_t batch, const float* params_in, float* params_out,
+                             const float* mom_in, float* mom_out, float* grads, float momentum,
+                             float wd, const float* lr, uint32_t update_batch, float* sq_err,
+                             void* ws, size_t ws_bytes, srcnn_stream_t stream) {
+  SRCNN_REQUIRE(net && params_in && grads, "train_fwd_bwd_lazy: null argument");
+  size_t off[6];
+  if (int rc = srcnn_net_offsets(net, off)) return rc;
+  const size_t total = off[5] + 1;
+  SRCNN_REQUIRE(total < (1ull << 32), "train_fwd_bwd_lazy: parameter count %zu too large", total);
+  srcnn::fused::LazyUpdate u{};
+  u.P = params_in;
+  u.G = grads;
+  if (update_batch > 0) {
+    SRCNN_REQUIRE(params_out && mom_in && mom_out && lr, "train_fwd_bwd_lazy: null argument");
+    // out of place: the blocks of the first kernel read the old values while
+    // others write the new ones
+    auto disjoint = [total](const float* a, const float* b) { return a + total <= b || b + total <= a; };
+    SRCNN_REQUIRE(disjoint(params_in, params_out) && disjoint(mom_in, mom_out) &&
+                      disjoint(params_out, mom_out) && disjoint(grads, params_out) && disjoint(grads, mom_out),
+                  "train_fwd_bwd_lazy: params_in / params_out / mom_in / mom_out / grads overlap");
+    u.M = mom_in;
+    u.Po = params_out;
+    u.Mo = mom_out;
+    for (int k = 0; k < 6; k++) u.off[k] = (uint32_t)off[k];
+    u.off[6] = (uint32_t)total;
+    for (int k = 0; k < 3; k++) u.lr[k] = lr[k];
+    u.mu = momentum;
+    u.wd = wd;
+    u.batch = (float)update_batch;
+  }
+  if (batch == 0) {  // no tiles: the pending update alone, gradients zero
+    if (update_batch == 0) return srcnn_fill_f32(grads, 0.0f, total, stream);
+    return srcnn::lazy_update(u, srcnn::as_stream(stream));
+  }
+  return train_impl(net, X, T, w, h, batch, params_in, grads, sq_err, ws, ws_bytes, stream, nullptr,
+                    nullptr, &u);
 }
 
 int srcnn_train_activations(const srcnn_net* net, uint32_t w, uint32_t h, uint32_t batch,

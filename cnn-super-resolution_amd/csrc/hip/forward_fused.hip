@@ -139,7 +139,6 @@ __global__ __launch_bounds__(256, SRCNN_FWD_WAVES) void fwd_l123_kernel(
   for (int t = 0; t < NT1; t++)
 #pragma unroll
     for (int s = 0; s < 16; s++) w2f[t][s] = li < N2 ? W2[(32 * t + crow(s, h)) * N2 + li] : 0.0f;
-  const float b2a = (h == 0 && li < N2) ? B2[li] : 0.0f;
   if (threadIdx.x < 32) {
     const int c_ = crow(threadIdx.x & 15, threadIdx.x >> 4);
     b2i[threadIdx.x >> 4][threadIdx.x & 15] = c_ < N2 ? B2[c_] : 0.0f;
@@ -224,15 +223,11 @@ __global__ __launch_bounds__(256, SRCNN_FWD_WAVES) void fwd_l123_kernel(
           if (!(kFwdDiag & 4)) acc1[t][r] = fmaxf(acc1[t][r], 0.0f);
       // L2^T: A2^T[n][p] = B2[n] + sum_c W2[c][n] A1^T[c][p], then ReLU
       f32x16 acc2;
-      if (SRCNN_B2_INIT) {
-      #pragma unroll
-        for (int q = 0; q < 4; q++) {
-          const mfma::f32x4 v_ = *reinterpret_cast<const mfma::f32x4*>(&b2i[h][4 * q]);
-      #pragma unroll
-          for (int e = 0; e < 4; e++) acc2[4 * q + e] = v_[e];
-        }
-      } else {
-        acc2 = mma(b2a, 1.0f, zero16());
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const mfma::f32x4 v_ = *reinterpret_cast<const mfma::f32x4*>(&b2i[h][4 * q]);
+#pragma unroll
+        for (int e = 0; e < 4; e++) acc2[4 * q + e] = v_[e];
       }
 #pragma unroll
       for (int t = 0; t < NT1; t++)

@@ -15,13 +15,9 @@
 
 #include <hip/hip_runtime.h>
 
-// L2 bias of l12 / fwd_l123 as the accumulator's initial value (1, default)
-// or as one more MFMA per 32-pixel chunk (0, A/B).  Same-box A/B
-// (profiles/r04_ab_b2init): l12 0.3051 -> 0.3040 ms, 3840x2160 frame
-// 1.134 -> 1.112 ms; bit-identical results (the chain starts from B2 either way)
-#ifndef SRCNN_B2_INIT
-#define SRCNN_B2_INIT 1
-#endif
+// (l12 / fwd_l123 start the L2 accumulator from B2 instead of one more MFMA
+// per 32-pixel chunk: l12 0.3051 -> 0.3040 ms, 3840x2160 frame 1.134 ->
+// 1.112 ms, bit-identical; profiles/r04_ab_b2init)
 
 namespace srcnn {
 namespace mfma {

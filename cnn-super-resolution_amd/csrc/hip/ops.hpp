@@ -43,13 +43,18 @@ int try_conv_grad_acc(const float* in, const float* d, float* gW, float* gB, uin
 // query_only the slab workspace size written to *need), 0 when not.
 namespace fused {
 struct SlabUpdate;
+struct LazyUpdate;
 // With `up` (srcnn_train_step) the slab reduction also applies the SGD
 // update to every parameter it completes and returns 2 instead of 1 when it
-// did (layer 3 on l3_delta, so the slabs cover all parameters).
+// did (layer 3 on l3_delta, so the slabs cover all parameters).  With `lz`
+// (srcnn_train_fwd_bwd_lazy) the step first applies lz's pending update
+// inside l12 (lz->batch > 0; `params` is then ignored and the step runs on
+// lz->Po) and OVERWRITES grads instead of accumulating.
 int train_fwd_bwd(const srcnn_net* net, const float* X, const float* T, uint32_t w, uint32_t h,
                   uint32_t batch, const float* params, float* grads, float* sq_err, float* A1,
                   float* A2, float* D2, float* A3, float* D3, float* slab, size_t slab_bytes,
-                  hipStream_t s, bool query_only, size_t* need, const SlabUpdate* up = nullptr);
+                  hipStream_t s, bool query_only, size_t* need, const SlabUpdate* up = nullptr,
+                  const LazyUpdate* lz = nullptr);
 // Fused inference (forward_fused.hip): 1 when specialised (with query_only:
 // workspace bytes in *need), 0 when not.
 int forward(const srcnn_net* net, const float* X, uint32_t w, uint32_t h, uint32_t batch,
@@ -76,7 +81,9 @@ struct SlabUpdate {
   float mu, wd, batch;
   int nseg;
 };
-int reduce_slabs(const SlabSeg* segs, int nseg, hipStream_t s, const SlabUpdate* up = nullptr);
+// assign: segments k < assign are written (dst = sum) instead of accumulated
+int reduce_slabs(const SlabSeg* segs, int nseg, hipStream_t s, const SlabUpdate* up = nullptr,
+                 int assign = 0);
 // SGD-momentum step of one parameter (update_parameters.cl:14-32): segment
 // seg of [W1|B1|W2|B2|W3|B3], weights with weight decay, biases without;
 // w, m = parameter and momentum in, out.  Shared by update_all_kernel and the
@@ -93,6 +100,42 @@ __device__ __forceinline__ void sgd_step(float& w, float& m, int seg, float g, f
     const float db = mu * m + lr * g;
     w -= db / batch;
     m = db;
+  }
+}
+// The previous data-parallel step's update, applied out of place by the next
+// step's first kernel (srcnn_train_fwd_bwd_lazy): Po = sgd(P, M, G),
+// Mo likewise, with sgd_step's arithmetic.  batch == 0: no pending update.
+struct LazyUpdate {
+  const float *P, *M, *G;
+  float *Po, *Mo;
+  uint32_t off[7];  // [W1|B1|W2|B2|W3|B3] offsets, off[6] = total
+  float lr[3];
+  float mu, wd, batch;
+};
+// segment of flat parameter index i
+__device__ __forceinline__ int param_seg(const uint32_t* off, uint32_t i) {
+  int seg = 0;
+#pragma unroll
+  for (int k = 1; k < 6; k++) seg += i >= off[k];
+  return seg;
+}
+// updated value of parameter off[seg] + i
+__device__ __forceinline__ float lazy_param(const LazyUpdate& u, int seg, uint32_t i) {
+  const uint32_t gi = u.off[seg] + i;
+  float w = u.P[gi], m = u.M[gi];
+  sgd_step(w, m, seg, u.G[gi], u.lr[seg >> 1], u.mu, u.wd, u.batch);
+  return w;
+}
+// this block's slice of Po / Mo (the slices of a grid cover every parameter)
+__device__ __forceinline__ void lazy_write_slice(const LazyUpdate& u) {
+  const uint32_t n = u.off[6], per = (n + gridDim.x - 1) / gridDim.x;
+  const uint32_t b0 = blockIdx.x * per, e = min(n, b0 + per);
+  for (uint32_t i = b0 + threadIdx.x; i < e; i += blockDim.x) {
+    const int seg = param_seg(u.off, i);
+    float w = u.P[i], m = u.M[i];
+    sgd_step(w, m, seg, u.G[i], u.lr[seg >> 1], u.mu, u.wd, u.batch);
+    u.Po[i] = w;
+    u.Mo[i] = m;
   }
 }
 // held-clock probes (common.hpp): slot 0 l12_fwd, 1 l3_delta, 2 d1_grad12
@@ -148,6 +191,9 @@ int fill(float* d, float v, size_t n, hipStream_t s);
 int preload_update();
 int update_all(float* params, float* grads, float* mom, const size_t* off, size_t total,
                const float* lr, float mu, float wd, uint32_t batch, hipStream_t s);
+// srcnn_train_fwd_bwd_lazy off the fused path: u.Po / u.Mo = the pending
+// update of u.P / u.M by u.G (update_all's arithmetic), then G = 0
+int lazy_update(const fused::LazyUpdate& u, hipStream_t s);
 int extract_luma(const uint8_t* rgba, float* luma, uint32_t w, uint32_t h, int normalize,
                  hipStream_t s);
 int swap_luma(const uint8_t* rgba, const float* nl, uint8_t* rgb, uint32_t w, uint32_t h,

@@ -293,9 +293,30 @@ int update_all(float* params, float* grads, float* mom, const size_t* off, size_
   return SRCNN_OK;
 }
 
+// srcnn_train_fwd_bwd_lazy off the fused path: the pending update out of
+// place (Po, Mo), then the gradient buffer zeroed for the step's accumulation
+__global__ void lazy_update_kernel(fused::LazyUpdate u) {
+  float* G = const_cast<float*>(u.G);
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < u.off[6]; i += gridDim.x * blockDim.x) {
+    const int seg = fused::param_seg(u.off, i);
+    float w = u.P[i], m = u.M[i];
+    fused::sgd_step(w, m, seg, G[i], u.lr[seg >> 1], u.mu, u.wd, u.batch);
+    u.Po[i] = w;
+    u.Mo[i] = m;
+    G[i] = 0.0f;
+  }
+}
+
+int lazy_update(const fused::LazyUpdate& u, hipStream_t s) {
+  SRCNN_PROFILE("update_all", s);
+  hipLaunchKernelGGL(lazy_update_kernel, dim3(grid_for(u.off[6], 256, 2048)), dim3(256), 0, s, u);
+  SRCNN_LAUNCH_TRY();
+  return SRCNN_OK;
+}
+
 int preload_update() {
-  const void* k[] = {(const void*)update_all_kernel};
-  return resolve_kernels(k, 1);
+  const void* k[] = {(const void*)update_all_kernel, (const void*)lazy_update_kernel};
+  return resolve_kernels(k, 2);
 }
 
 // ---------------------------------------------------------------------------

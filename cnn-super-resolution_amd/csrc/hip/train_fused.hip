@@ -76,9 +76,6 @@ struct Geom {
 // held-clock probe slots (common.hpp): 0 l12_fwd, 1 l3_delta, 2 d1_grad12
 __device__ unsigned long long g_clk[3][kClockBlocks][2];
 
-#ifndef SRCNN_L12_W1LDS
-#define SRCNN_L12_W1LDS 0
-#endif
 #ifndef SRCNN_L12_GRID
 #define SRCNN_L12_GRID 512  // grid cap (blocks) = 256 CUs x 2 resident blocks: the samples are
                             // written in index order, which l3 reads back in reverse (MALL)
@@ -123,11 +120,18 @@ constexpr int kL12A2S = 36;  // A2 scratch row stride (floats)
 #ifndef SRCNN_L12_WAVES
 #define SRCNN_L12_WAVES 2  // minimum waves per SIMD (register budget 512 / this)
 #endif
-template <int N1, int N2, int F1>
+// kLazy (srcnn_train_fwd_bwd_lazy): the previous data-parallel step's SGD
+// update rides in the prologue.  Every block forms the updated W1 / B1 / W2 /
+// B2 it needs in registers from lz's (P, M, G) -- the same sgd_step as
+// update_all_kernel, so every block holds the same values -- and writes its
+// slice of the updated parameters and momentum (all six segments) to lz.Po /
+// lz.Mo, which l3 and d1 read after this kernel.  No update launch between
+// the gradient all-reduce and the next step.
+template <int N1, int N2, int F1, bool kLazy = false>
 __global__ __launch_bounds__(256, SRCNN_L12_WAVES) void l12_fwd_kernel(
     const float* __restrict__ X, const float* __restrict__ W1, const float* __restrict__ B1,
     const float* __restrict__ W2, const float* __restrict__ B2, float* __restrict__ A1,
-    float* __restrict__ A2, Geom g) {
+    float* __restrict__ A2, Geom g, LazyUpdate lz) {
   constexpr int K1 = F1 * F1, KS1 = (K1 + 1) / 2, NT1 = N1 / 32;
   static_assert(N2 <= 32 && N2 % 8 == 0 && K1 % 2 == 1 && N1 % 32 == 0,
                 "transposed l12: one 32-row L2 tile, odd tap count");
@@ -144,37 +148,47 @@ __global__ __launch_bounds__(256, SRCNN_L12_WAVES) void l12_fwd_kernel(
   const int h = lane >> 5, li = lane & 31;
   const int npx = g.ow * g.oh;
   const int nch = (npx + 31) / 32;
+  // kLazy: the updated W1 | B1 | W2 | B2 (the flat buffer's first P12
+  // floats) are formed once per block into LDS, each by one thread with
+  // coalesced loads; the register operands below are read from there
+  constexpr int P12 = F1 * F1 * N1 + N1 + N1 * N2 + N2;
+  __shared__ float lzs[kLazy ? P12 : 1];
+  if constexpr (kLazy) {
+    lazy_write_slice(lz);
+    for (int i = threadIdx.x; i < P12; i += blockDim.x) {
+      const int seg = param_seg(lz.off, i);
+      float w_ = lz.P[i], m_ = lz.M[i];
+      sgd_step(w_, m_, seg, lz.G[i], lz.lr[seg >> 1], lz.mu, lz.wd, lz.batch);
+      lzs[i] = w_;
+    }
+    __syncthreads();
+  }
+  // parameter i of segment seg (W1 0, B1 1, W2 2, B2 3) as this step uses it
+  auto prm = [&](int seg, int i) -> float {
+    if constexpr (kLazy) return lzs[(seg > 0 ? K1 * N1 : 0) + (seg > 1 ? N1 : 0) + (seg > 2 ? N1 * N2 : 0) + i];
+    return (seg == 0 ? W1 : seg == 1 ? B1 : seg == 2 ? W2 : B2)[i];
+  };
 
   // A operands of L1^T: W1[tap = 2s + h][ch = 32t + li]; tap K1 is the bias slot
-#if SRCNN_L12_W1LDS
-  // read from LDS at each MFMA (frees 2 * KS1 registers for a third wave per SIMD)
-  __shared__ float w1s[2 * KS1 * N1];
-  for (int i = threadIdx.x; i < 2 * KS1 * N1; i += blockDim.x) {
-    const int tap = i / N1, ch = i - tap * N1;
-    w1s[i] = tap < K1 ? W1[i] : (tap == K1 ? B1[ch] : 0.0f);
-  }
-#define SRCNN_W1F(S, T) w1s[w1o + 2 * (S) * N1 + 32 * (T)]
-#else
+  // (W1 in registers: read from LDS at each MFMA instead, for a third wave
+  // per SIMD, l12 ran 0.323-0.325 vs 0.307 ms)
   float w1f[KS1][NT1];
 #pragma unroll
   for (int s = 0; s < KS1; s++)
 #pragma unroll
     for (int t = 0; t < NT1; t++) {
       const int tap = 2 * s + h;
-      w1f[s][t] = tap < K1 ? W1[tap * N1 + 32 * t + li] : B1[32 * t + li];
+      w1f[s][t] = tap < K1 ? prm(0, tap * N1 + 32 * t + li) : prm(1, 32 * t + li);
     }
-#define SRCNN_W1F(S, T) w1f[S][T]
-#endif
   // A operands of L2^T: W2[c = 32t + crow(s, h)][n = li]; bias MFMA: B2[li] (half 0)
   float w2f[NT1][16];
 #pragma unroll
   for (int t = 0; t < NT1; t++)
 #pragma unroll
-    for (int s = 0; s < 16; s++) w2f[t][s] = li < N2 ? W2[(32 * t + crow(s, h)) * N2 + li] : 0.0f;
-  const float b2a = (h == 0 && li < N2) ? B2[li] : 0.0f;
+    for (int s = 0; s < 16; s++) w2f[t][s] = li < N2 ? prm(2, (32 * t + crow(s, h)) * N2 + li) : 0.0f;
   if (threadIdx.x < 32) {
     const int c_ = crow(threadIdx.x & 15, threadIdx.x >> 4);
-    b2i[threadIdx.x >> 4][threadIdx.x & 15] = c_ < N2 ? B2[c_] : 0.0f;
+    b2i[threadIdx.x >> 4][threadIdx.x & 15] = c_ < N2 ? prm(3, c_) : 0.0f;
   }
 
   // The next sample's X tile is register-staged during the current sample
@@ -260,11 +274,6 @@ __global__ __launch_bounds__(256, SRCNN_L12_WAVES) void l12_fwd_kernel(
       const int iy = pc / g.ow, ix = pc - iy * g.ow;
       const int xbA = iy * kL12S + ix + h, xbB = xbA + h * (kL12S - F1);
 
-#if SRCNN_L12_W1LDS
-      // opaque per chunk, so the W1 reads are not hoisted out of the loops
-      int w1o = h * N1 + li;
-      asm volatile("" : "+v"(w1o));
-#endif
       f32x16 acc1[NT1];
 #pragma unroll
       for (int t = 0; t < NT1; t++) acc1[t] = zero16();
@@ -288,7 +297,7 @@ __global__ __launch_bounds__(256, SRCNN_L12_WAVES) void l12_fwd_kernel(
         if (kL12PD > 0) __builtin_amdgcn_sched_barrier(0);
         const float xv = kL12PD > 0 ? xq[s] : xg(s);
 #pragma unroll
-        for (int t = 0; t < NT1; t++) acc1[t] = mma(SRCNN_W1F(s, t), xv, acc1[t]);
+        for (int t = 0; t < NT1; t++) acc1[t] = mma(w1f[s][t], xv, acc1[t]);
         if (s % kStoreEvery == kStoreEvery - 1 && s / kStoreEvery < NST) store_prev(s / kStoreEvery);
       }
       // ReLU (layer_uber_kernel.cl:88-95); the bias is already in
@@ -297,15 +306,11 @@ __global__ __launch_bounds__(256, SRCNN_L12_WAVES) void l12_fwd_kernel(
 #pragma unroll
         for (int r = 0; r < 16; r++) acc1[t][r] = fmaxf(acc1[t][r], 0.0f);
       f32x16 acc2;
-      if (SRCNN_B2_INIT) {
-      #pragma unroll
-        for (int q = 0; q < 4; q++) {
-          const f32x4 v_ = *reinterpret_cast<const f32x4*>(&b2i[h][4 * q]);
-      #pragma unroll
-          for (int e = 0; e < 4; e++) acc2[4 * q + e] = v_[e];
-        }
-      } else {
-        acc2 = mma(b2a, 1.0f, zero16());
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const f32x4 v_ = *reinterpret_cast<const f32x4*>(&b2i[h][4 * q]);
+#pragma unroll
+        for (int e = 0; e < 4; e++) acc2[4 * q + e] = v_[e];
       }
 #pragma unroll
       for (int t = 0; t < NT1; t++)
@@ -348,7 +353,6 @@ __global__ __launch_bounds__(256, SRCNN_L12_WAVES) void l12_fwd_kernel(
   }
   SRCNN_CLOCK_END(g_clk, 0);
 }
-#undef SRCNN_W1F
 
 #include "l3_delta.hpp"
 #include "l3r.hpp"
@@ -881,6 +885,7 @@ struct SlabSegs {
   SlabSeg seg[kMaxSlabSegs];
   int first[kMaxSlabSegs + 1];
   SlabUpdate up;  // up.nseg = 0: plain reduction
+  int assign;     // segments k < assign: dst = sum (srcnn_train_fwd_bwd_lazy) instead of dst += sum
 };
 
 __global__ __launch_bounds__(1024) void slab_reduce_kernel(SlabSegs ss) {
@@ -931,15 +936,18 @@ __global__ __launch_bounds__(1024) void slab_reduce_kernel(SlabSegs ss) {
       u.P[ui] = uw;
       u.M[ui] = um;
       u.G[ui] = 0.0f;
+    } else if (k < ss.assign) {
+      sg.dst[col] = t;
     } else {
       sg.dst[col] += t;
     }
   }
 }
 
-int reduce_slabs(const SlabSeg* segs, int nseg, hipStream_t s, const SlabUpdate* up) {
+int reduce_slabs(const SlabSeg* segs, int nseg, hipStream_t s, const SlabUpdate* up, int assign) {
   SlabSegs ss{};
   if (up) ss.up = *up;
+  ss.assign = assign;
   int blocks = 0;
   for (int k = 0; k < kMaxSlabSegs; k++) {
     ss.first[k] = blocks;
@@ -1005,7 +1013,7 @@ template <int N1, int N2, int F1, int F3>
 static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t batch,
                const float* params, float* grads, float* sq_err, float* A1, float* A2, float* D2,
                float* A3, float* D3, float* slab, size_t slab_bytes, hipStream_t s, bool query_only,
-               size_t* need, const SlabUpdate* up) {
+               size_t* need, const SlabUpdate* up, const LazyUpdate* lz) {
   using NetT = Net<N1, N2, F1, F3>;
   const int ow = w - F1 + 1, oh = h - F1 + 1;
   const int w3 = ow - F3 + 1, h3 = oh - F3 + 1;
@@ -1054,6 +1062,9 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   float* slab12 = slab;
   float* slab3 = slab12 + s12;
   float* sqs = slab3 + s3;
+  // lazy: l12 applies the pending update and the step runs on lz->Po
+  const bool lazy = lz && lz->batch > 0.0f;
+  if (lazy) params = lz->Po;
   // flat parameter layout [W1|B1|W2|B2|W3|B3]
   const float* W1 = params;
   const float* B1 = W1 + F1 * F1 * N1;
@@ -1064,10 +1075,18 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   Geom g{(int)w, (int)h, ow, oh, (int)batch};
   {
     SRCNN_PROFILE("l12_fwd_mfma", s);
-    hipLaunchKernelGGL((l12_fwd_kernel<N1, N2, F1>), dim3(g12), dim3(256), 0, s, X, W1,
-                       B1, W2, B2, A1, A2, g);
+    if (lazy)
+      hipLaunchKernelGGL((l12_fwd_kernel<N1, N2, F1, true>), dim3(g12), dim3(256), 0, s, X, W1,
+                         B1, W2, B2, A1, A2, g, *lz);
+    else
+      hipLaunchKernelGGL((l12_fwd_kernel<N1, N2, F1>), dim3(g12), dim3(256), 0, s, X, W1,
+                         B1, W2, B2, A1, A2, g, LazyUpdate{});
     SRCNN_LAUNCH_TRY();
   }
+  // lazy, layer 3 on the op-level kernels: they accumulate, so their
+  // gradient segment starts from zero (after l12 has read the pending one)
+  if (lz && !l3_fused)
+    SRCNN_HIP_TRY(hipMemsetAsync(grads + NetT::P12, 0, NetT::P3 * sizeof(float), s));
   L3Geom lg{(int)w, (int)h, ow, oh, w3, h3, (int)batch};
   if (l3_fused) {
     SRCNN_PROFILE("l3_delta_fused", s);
@@ -1110,7 +1129,9 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
       u = *up;
       u.nseg = 2;
     }
-    int rc = l3_fused ? reduce_slabs(segs, sq_err ? 3 : 2, s, &u) : reduce_slabs(segs, 1, s);
+    // lazy: the slabs are this step's whole gradient (assigned, not added)
+    const int assign = lz ? (l3_fused ? 2 : 1) : 0;
+    int rc = l3_fused ? reduce_slabs(segs, sq_err ? 3 : 2, s, &u, assign) : reduce_slabs(segs, 1, s, nullptr, assign);
     if (rc) return rc;
     if (up && l3_fused) return 2;
   }
@@ -1122,12 +1143,12 @@ static int dispatch_one(const srcnn_net* net, const float* X, const float* T, ui
                         uint32_t h, uint32_t batch, const float* params, float* grads,
                         float* sq_err, float* A1, float* A2, float* D2, float* A3, float* D3,
                         float* slab, size_t slab_bytes, hipStream_t s, bool query_only,
-                        size_t* need, const SlabUpdate* up) {
+                        size_t* need, const SlabUpdate* up, const LazyUpdate* lz) {
   if (net->n1 != (uint32_t)N1 || net->n2 != (uint32_t)N2 || net->f1 != (uint32_t)F1 ||
       net->f2 != 1 || net->f3 != (uint32_t)F3)
     return 0;
   return run<N1, N2, F1, F3>(X, T, w, h, batch, params, grads, sq_err, A1, A2, D2, A3, D3, slab,
-                             slab_bytes, s, query_only, need, up);
+                             slab_bytes, s, query_only, need, up, lz);
 }
 
 template <int N1, int N2, int F1, int F3>
@@ -1135,10 +1156,11 @@ static int preload_one(const srcnn_net* net) {
   if (net->n1 != (uint32_t)N1 || net->n2 != (uint32_t)N2 || net->f1 != (uint32_t)F1 ||
       net->f2 != 1 || net->f3 != (uint32_t)F3)
     return 0;
-  const void* k[] = {(const void*)l12_fwd_kernel<N1, N2, F1>, (const void*)l3_delta_kernel<N2, F3>,
-                     (const void*)d1_grad12_kernel<N1, N2, F1>, (const void*)slab_reduce_kernel,
-                     (const void*)l3r_delta_kernel<F3>, (const void*)d1c_grad12_kernel<9>};
-  int rc = resolve_kernels(k, SRCNN_D1C && N1 == 64 && N2 == 32 && F1 == 9 ? 6 : 5);
+  const void* k[] = {(const void*)l12_fwd_kernel<N1, N2, F1>, (const void*)l12_fwd_kernel<N1, N2, F1, true>,
+                     (const void*)l3_delta_kernel<N2, F3>, (const void*)d1_grad12_kernel<N1, N2, F1>,
+                     (const void*)slab_reduce_kernel, (const void*)l3r_delta_kernel<F3>,
+                     (const void*)d1c_grad12_kernel<9>};
+  int rc = resolve_kernels(k, SRCNN_D1C && N1 == 64 && N2 == 32 && F1 == 9 ? 7 : 6);
   return rc ? rc : 1;
 }
 
@@ -1188,11 +1210,12 @@ int train_clock(int slot, double* ghz) {
 int train_fwd_bwd(const srcnn_net* net, const float* X, const float* T, uint32_t w, uint32_t h,
                   uint32_t batch, const float* params, float* grads, float* sq_err, float* A1,
                   float* A2, float* D2, float* A3, float* D3, float* slab, size_t slab_bytes,
-                  hipStream_t s, bool query_only, size_t* need, const SlabUpdate* up) {
+                  hipStream_t s, bool query_only, size_t* need, const SlabUpdate* up,
+                  const LazyUpdate* lz) {
   int rc;
-#define SRCNN_FUSED_CASE(n1, n2, f1, f3)                                                         \
-  if ((rc = dispatch_one<n1, n2, f1, f3>(net, X, T, w, h, batch, params, grads, sq_err, A1, A2,  \
-                                         D2, A3, D3, slab, slab_bytes, s, query_only, need, up)) != 0) \
+#define SRCNN_FUSED_CASE(n1, n2, f1, f3)                                                             \
+  if ((rc = dispatch_one<n1, n2, f1, f3>(net, X, T, w, h, batch, params, grads, sq_err, A1, A2,      \
+                                         D2, A3, D3, slab, slab_bytes, s, query_only, need, up, lz)) != 0) \
     return rc;
   SRCNN_FUSED_CASE(64, 32, 9, 5)  // reference default (BASELINE.json configs[1])
   SRCNN_FUSED_CASE(32, 16, 9, 5)  // example_config.json

@@ -89,7 +89,9 @@ SIGNATURES = {
     "srcnn_update_all": (_I, [_NP, _P, _P, _P, _F, _F, ctypes.POINTER(_F), _U, _P]),
     "srcnn_train_step": (_I, [_NP, _P, _P, _U, _U, _U, _P, _P, _P, _F, _F, ctypes.POINTER(_F), _U,
                               _P, _P, _S, _P]),
-    "srcnn_train_activations": (_I, [_NP, _U, _U, _U, _P, _S, _P, _P, _P, _P]),
+    "srcnn_train_fwd_bwd_lazy": (_I, [_NP, _P, _P, _U, _U, _U, _P, _P, _P, _P, _P, _F, _F,
+                                      ctypes.POINTER(_F), _U, _P, _P, _S, _P]),
+    "srcnn_train_activations":(_I, [_NP, _U, _U, _U, _P, _S, _P, _P, _P, _P]),
     "srcnn_preload": (_I, [_NP]),
     "srcnn_forward_workspace_bytes": (_S, [_NP, _U, _U, _U]),
     "srcnn_forward": (_I, [_NP, _P, _U, _U, _U, _P, _P, _P, _S, _P]),
@@ -334,6 +336,17 @@ def train_step(net, X, T, w, h, batch, params, grads, mom, momentum, wd, lr, upd
     _call("srcnn_train_step", ctypes.byref(net), ptr(X), ptr(T), w, h, batch, ptr(params),
           ptr(grads), ptr(mom), momentum, wd, lr_arr, update_batch, ptr(sq_err_dev), ptr(ws),
           ws_bytes, s)
+
+
+def train_fwd_bwd_lazy(net, X, T, w, h, batch, params_in, params_out, mom_in, mom_out, grads,
+                       momentum, wd, lr, update_batch, sq_err_dev, ws, ws_bytes, s=None):
+    """srcnn_train_fwd_bwd_lazy: the pending update of `grads` (update_batch
+    > 0) out of place into params_out / mom_out, then this step's gradients
+    over the batch on the updated parameters, written to `grads`."""
+    lr_arr = (_F * 3)(*lr)
+    _call("srcnn_train_fwd_bwd_lazy", ctypes.byref(net), ptr(X), ptr(T), w, h, batch, ptr(params_in),
+          ptr(params_out), ptr(mom_in), ptr(mom_out), ptr(grads), momentum, wd, lr_arr, update_batch,
+          ptr(sq_err_dev), ptr(ws), ws_bytes, s)
 
 
 class Graph:

@@ -24,6 +24,7 @@ The collective is injected too.  Two implementations:
                  "nccl"; gloo in the CPU tests and the one-GPU rehearsal)
 """
 import contextlib
+import datetime
 import os
 import sys
 
@@ -52,13 +53,19 @@ def _stdout_to_stderr():
         os.close(saved)
 
 
-def init(backend, device=None):
-    """init_process_group from the env (MASTER_ADDR defaults to 127.0.0.1)."""
+def init(backend, device=None, timeout_s=None):
+    """init_process_group from the env (MASTER_ADDR defaults to 127.0.0.1).
+    Collectives of the group time out after `timeout_s` (default
+    SRCNN_DIST_TIMEOUT_S or 600 s) instead of torch's 30 minutes, so a rank
+    left waiting on a peer that died fails instead of hanging."""
     rank, world, _ = env_world()
     if world <= 1:
         return rank, world
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if timeout_s is None:
+        timeout_s = float(os.environ.get("SRCNN_DIST_TIMEOUT_S", "600"))
     kw = {"device_id": device} if device is not None and backend == "nccl" else {}
+    kw["timeout"] = datetime.timedelta(seconds=timeout_s)
     with _stdout_to_stderr():
         dist.init_process_group(backend, rank=rank, world_size=world, **kw)
         dist.barrier()  # gloo connects its mesh lazily on some versions
@@ -158,3 +165,59 @@ class DataParallelStep:
         self.fwd_bwd(self.grads)
         self.allreduce()
         self.update(self.global_batch)
+
+
+class LazyDataParallelStep:
+    """The same data-parallel training, one launch shorter per step: step t's
+    SGD update is applied by step t + 1's first kernel
+    (srcnn_train_fwd_bwd_lazy), so a step is
+        fwd_bwd_lazy(p_in, p_out, m_in, m_out, grads, pending) -> allreduce(grads)
+    with the parameter and momentum buffers ping-ponged (the update is out of
+    place: every block of the first kernel reads the old values).  `pending`
+    is the global batch of the update still owed (0 before the first step);
+    `finish()` applies it (srcnn_update_all on the current buffers) and
+    returns them.  Bit-identical to DataParallelStep's fwd_bwd -> allreduce ->
+    update sequence.
+
+    fwd_bwd_lazy(p_in, p_out, m_in, m_out, grads, pending) and
+    update(params, mom, grads, batch) are injected as in DataParallelStep."""
+
+    def __init__(self, params, params2, mom, mom2, grads, fwd_bwd_lazy, update, global_batch,
+                 group=None, allreduce=None):
+        for t in (params, params2, mom, mom2, grads):
+            if not isinstance(t, torch.Tensor) or t.dtype != torch.float32:
+                raise TypeError("parameter, momentum and gradient buffers must be float32 tensors")
+        self.P = [params, params2]
+        self.M = [mom, mom2]
+        self.grads = grads
+        self.fwd_bwd_lazy = fwd_bwd_lazy
+        self.update = update
+        self.global_batch = int(global_batch)
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        self._allreduce = allreduce
+        self.cur = 0        # index of the buffers holding the current parameters
+        self.pending = 0    # batch of the update not yet applied (0: none)
+
+    def allreduce(self):
+        if self.world <= 1:
+            return
+        if self._allreduce is not None:
+            self._allreduce(self.grads)
+        else:
+            dist.all_reduce(self.grads, op=dist.ReduceOp.SUM, group=self.group)
+
+    def __call__(self):
+        i, o = self.cur, 1 - self.cur
+        self.fwd_bwd_lazy(self.P[i], self.P[o], self.M[i], self.M[o], self.grads, self.pending)
+        if self.pending:
+            self.cur = o
+        self.allreduce()
+        self.pending = self.global_batch
+
+    def finish(self):
+        """Apply the owed update; returns (params, momentum) now current."""
+        if self.pending:
+            self.update(self.P[self.cur], self.M[self.cur], self.grads, self.pending)
+            self.pending = 0
+        return self.P[self.cur], self.M[self.cur]

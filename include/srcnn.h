@@ -324,6 +324,34 @@ SRCNN_API int srcnn_comm_version(int* version, char* path, size_t len);
 SRCNN_API int srcnn_allreduce_grads(srcnn_comm_t comm, float* buf, size_t count,
                                     srcnn_stream_t stream);
 
+/* The data-parallel step without an update launch (an MI355X extension of
+ * src/Main_cl.cpp:161-175 / src/ConfigBasedDataPipeline.cpp:325-361, where
+ * update_parameters follows execute_batch): the update of step t is applied by
+ * the first kernel of step t + 1.  With update_batch > 0 the call first applies
+ * the pending update of `grads` (the previous step's all-reduced gradients)
+ * OUT OF PLACE -- params_out / mom_out = srcnn_update_all's arithmetic on
+ * params_in / mom_in / grads with batch = update_batch -- then runs
+ * srcnn_train_fwd_bwd on params_out and OVERWRITES grads with this step's
+ * gradients.  With update_batch == 0 (nothing pending) it runs on params_in,
+ * writes neither params_out nor mom_out (they may be NULL) and overwrites
+ * grads.  A data-parallel step is then
+ *     srcnn_train_fwd_bwd_lazy (ping-ponging two parameter / momentum buffers)
+ *     srcnn_allreduce_grads
+ * and srcnn_update_all(current params, grads, current momentum) applies the
+ * last pending update.  The sequence is bit-identical to srcnn_train_fwd_bwd
+ * (on zeroed grads) + srcnn_allreduce_grads + srcnn_update_all per step.  On
+ * the fused path (nets with f2 == 1) the update runs in the prologue of the
+ * first kernel; elsewhere one update launch precedes the step.  params_in,
+ * params_out, mom_out and grads must not overlap (SRCNN_ERR_INVALID). */
+SRCNN_API int srcnn_train_fwd_bwd_lazy(const srcnn_net* net, const float* X,
+                                       const float* T, uint32_t w, uint32_t h,
+                                       uint32_t batch, const float* params_in,
+                                       float* params_out, const float* mom_in,
+                                       float* mom_out, float* grads, float momentum,
+                                       float wd, const float* lr, uint32_t update_batch,
+                                       float* sq_err, void* ws, size_t ws_bytes,
+                                       srcnn_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -71,9 +71,25 @@ def main():
         dist.all_reduce(h, op=dist.ReduceOp.SUM)
         g.copy_(h.to(dev))
 
-    step = parallel.DataParallelStep(grads, fwd_bwd, update, gb, allreduce=allreduce)
+    if os.environ.get("SRCNN_DP_LAZY"):
+        # bench.py's N > 1 step: srcnn_train_fwd_bwd_lazy (ping-ponged
+        # parameters, the previous update inside the first kernel) + all-reduce
+        def fwd_bwd_lazy(pi, po, mi, mo, g, pending):
+            S.train_fwd_bwd_lazy(net, Xd, Td, tile, tile, count, pi, po, mi, mo, g, 0.9, 1e-3, LR,
+                                 pending, None, ws, nbytes)
+            paths.append(S.last_path())
+
+        def update_lazy(p, m, g, nb):
+            S.update_all(net, p, g, m, 0.9, 1e-3, LR, nb)
+
+        step = parallel.LazyDataParallelStep(params, torch.empty_like(params), mom, torch.empty_like(mom),
+                                             grads, fwd_bwd_lazy, update_lazy, gb, allreduce=allreduce)
+    else:
+        step = parallel.DataParallelStep(grads, fwd_bwd, update, gb, allreduce=allreduce)
     for _ in range(steps):
         step()
+    if os.environ.get("SRCNN_DP_LAZY"):
+        params, mom = step.finish()
     torch.cuda.synchronize()
     np.save(os.path.join(out_dir, "params_%d.npy" % rank), params.cpu().numpy())
     with open(os.path.join(out_dir, "path_%d.txt" % rank), "w") as fh:

@@ -72,6 +72,68 @@ def _train(rank, world, global_batch, port, out_dir):
         torch.distributed.destroy_process_group()
 
 
+def _train_lazy(rank, world, global_batch, port, out_dir):
+    """The same training with parallel.LazyDataParallelStep: each step's
+    update applied out of place by the next step (srcnn_train_fwd_bwd_lazy's
+    contract, here on the oracle), finish() applying the last one."""
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import srcnn_oracle as orc
+    from srcnn_amd import parallel
+    orc.set_threads(1)
+    parallel.init("gloo")
+    X, T, p0 = _data(global_batch)
+    start, count = parallel.shard(global_batch, rank, world)
+    tile = W * H
+    Xs, Ts = X[start * tile:(start + count) * tile], T[start * tile:(start + count) * tile]
+    P = p0.size
+    bufs = [torch.from_numpy(p0.copy()), torch.full((P,), float("nan")),
+            torch.zeros(P), torch.full((P,), float("nan"))]
+    grads = torch.full((P,), float("nan"))  # overwritten by every step
+
+    def fwd_bwd_lazy(pi, po, mi, mo, g, pending):
+        cur = pi
+        if pending:
+            p, _, m = orc.update_all(NET, pi.numpy().copy(), g.numpy().copy(), mi.numpy().copy(),
+                                     0.9, 1e-3, LR, pending)
+            po.copy_(torch.from_numpy(p))
+            mo.copy_(torch.from_numpy(m))
+            cur = po
+        new = np.zeros(P, np.float32)
+        if count:
+            new, _ = orc.train_fwd_bwd(NET, Xs, Ts, W, H, count, cur.numpy().copy(), new)
+        g.copy_(torch.from_numpy(new))
+
+    def update(p, m, g, nb):
+        pn, gz, mn = orc.update_all(NET, p.numpy().copy(), g.numpy().copy(), m.numpy().copy(),
+                                    0.9, 1e-3, LR, nb)
+        p.copy_(torch.from_numpy(pn))
+        m.copy_(torch.from_numpy(mn))
+        g.copy_(torch.from_numpy(gz))
+
+    step = parallel.LazyDataParallelStep(bufs[0], bufs[1], bufs[2], bufs[3], grads, fwd_bwd_lazy, update,
+                                         global_batch)
+    for _ in range(STEPS):
+        step()
+    p, _ = step.finish()
+    np.save(os.path.join(out_dir, "lazy_%d.npy" % rank), p.numpy())
+    torch.distributed.barrier()
+    torch.distributed.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,global_batch", [(2, 6), (3, 7)])
+def test_lazy_step_bit_identical_to_separate_update(tmp_path, world, global_batch):
+    """LazyDataParallelStep (the N > 1 bench step) against DataParallelStep:
+    the same parameters bit for bit after STEPS steps, on every rank."""
+    for fn in (_train, _train_lazy):
+        mp.start_processes(fn, args=(world, global_batch, _free_port(), str(tmp_path)),
+                           nprocs=world, join=True, start_method="spawn")
+    for r in range(world):
+        a = np.load(tmp_path / ("params_%d.npy" % r))
+        b = np.load(tmp_path / ("lazy_%d.npy" % r))
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
 def _single(global_batch):
     import srcnn_oracle as orc
     X, T, p = _data(global_batch)
