@@ -85,6 +85,8 @@ extern "C" {
 
 const char* srcnn_last_path(void) { return t_path; }
 
+const char* srcnn_last_kernels(void) { return srcnn::kernels_last(); }
+
 
 int srcnn_fill_f32(float* dst, float value, size_t count, srcnn_stream_t stream) {
   if (count == 0) return SRCNN_OK;
@@ -319,6 +321,7 @@ static int train_impl(const srcnn_net* net, const float* X, const float* T, uint
                       const srcnn::fused::LazyUpdate* lz = nullptr) {
   NetDims d;
   if (int rc = net_dims(net, w, h, &d)) return rc;
+  if (!lz) srcnn::kernels_reset();  // (the lazy entry resets before its update)
   if (batch == 0) return SRCNN_OK;
   SRCNN_REQUIRE(X && T && grads && ws && (params || (lz && lz->batch > 0.0f)), "train_fwd_bwd: null buffer");
   const size_t need = srcnn_train_workspace_bytes(net, w, h, batch);
@@ -418,6 +421,7 @@ int srcnn_train_step(const srcnn_net* net, const float* X, const float* T, uint3
                           &updated))
     return rc;
   if (updated) return SRCNN_OK;
+  srcnn::kernels_note("update_all");
   return srcnn_update_all(net, params, grads, momentum_bufs, momentum, wd, lr, update_batch, stream);
 }
 
@@ -427,6 +431,7 @@ int srcnn_train_fwd_bwd_lazy(const srcnn_net* net, const float* X, const float* 
                              float wd, const float* lr, uint32_t update_batch, float* sq_err,
                              void* ws, size_t ws_bytes, srcnn_stream_t stream) {
   SRCNN_REQUIRE(net && params_in && grads, "train_fwd_bwd_lazy: null argument");
+  srcnn::kernels_reset();
   size_t off[6];
   if (int rc = srcnn_net_offsets(net, off)) return rc;
   const size_t total = off[5] + 1;

@@ -14,6 +14,11 @@ namespace srcnn {
 // Records a thread-local message for srcnn_last_error() and returns `code`.
 int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
 void clear_error();
+// the kernels (by variant) of this thread's most recent network-level call,
+// comma-separated (srcnn_last_kernels)
+void kernels_reset();
+void kernels_note(const char* name);
+const char* kernels_last();
 
 // hipFuncGetAttributes on each kernel: the runtime's lazy per-device kernel
 // setup happens here instead of at the first launch (srcnn_preload)

@@ -39,24 +39,11 @@
 // M0 is written by the DMA asm only; the compiler sets it itself around its own uses
 #pragma clang diagnostic ignored "-Winline-asm"
 
-#ifndef SRCNN_D1C_TEAMS
-#define SRCNN_D1C_TEAMS 1  // 4-wave teams per block, on alternate chunks of a sample
-#endif
-constexpr int kD1cTeams = SRCNN_D1C_TEAMS;
-// diagnostics builds only (results invalid): 1 no chunk barrier, 2 no chunk
-// operand DMA, 4 gW1 A operands from a register (no X gathers), 8 no relu' reads, 16 no slab write
-#ifdef SRCNN_D1C_DIAG
-constexpr int kD1cDiag = SRCNN_D1C_DIAG;
-#else
-constexpr int kD1cDiag = 0;
-#endif
-#ifndef SRCNN_D1C_OCC
-#define SRCNN_D1C_OCC 4  // waves per SIMD (launch bound; register budget 512 / this)
-#endif
-#ifndef SRCNN_D1C_GRID
-#define SRCNN_D1C_GRID (256 * SRCNN_D1C_OCC / SRCNN_D1C_TEAMS)  // all blocks resident
-#endif
-constexpr int kD1cGrid = SRCNN_D1C_GRID;
+// 4-wave teams per block, on alternate chunks of a sample (two teams per
+// block, 512 slabs instead of 1024: d1 0.4065 vs 0.399 ms)
+constexpr int kD1cTeams = 1;
+constexpr int kD1cOcc = 4;                           // waves per SIMD (launch bound: 128 VGPRs)
+constexpr int kD1cGrid = 256 * kD1cOcc / kD1cTeams;  // all blocks resident
 constexpr int kD1cS = 40;       // X tile row stride in LDS (8 mod 32)
 constexpr int kD1cMaxPx = 1024; // pixel slots of the X offset table (nch * 32)
 
@@ -91,7 +78,7 @@ inline size_t d1c_lds_bytes(int w, int h) {
 }
 
 template <int F1>
-__global__ __launch_bounds__(256 * kD1cTeams, SRCNN_D1C_OCC) void d1c_grad12_kernel(const float* __restrict__ X,
+__global__ __launch_bounds__(256 * kD1cTeams, kD1cOcc) void d1c_grad12_kernel(const float* __restrict__ X,
                                                             const float* __restrict__ A1,
                                                             const float* __restrict__ D2,
                                                             const float* __restrict__ W2,
@@ -213,10 +200,9 @@ __global__ __launch_bounds__(256 * kD1cTeams, SRCNN_D1C_OCC) void d1c_grad12_ker
       // this chunk's operands (and at cc == c_beg this item's X tile) have
       // landed for every wave; every wave is done with the other buffer
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (!(kD1cDiag & 1) || cc == c_beg) __syncthreads();
+      __syncthreads();
       const int c = cc + team;
-      if (kD1cDiag & 2) {
-      } else if (c + NT < c_end)
+      if (c + NT < c_end)
         dma_chunk(smp, c + NT, buf ^ 1);
       else if (nit < nitems && first_chunk(nit) + team < end_chunk(nit))
         dma_chunk(nit / parts, first_chunk(nit) + team, buf ^ 1);
@@ -233,7 +219,7 @@ __global__ __launch_bounds__(256 * kD1cTeams, SRCNN_D1C_OCC) void d1c_grad12_ker
       for (int pm = 0; pm < 2; pm++)
 #pragma unroll
         for (int i = 0; i < 4; i++)
-          mk[pm][i] = (kD1cDiag & 8) ? 1.0f : a1b[256 * pm + 16 * i + ((i & 1) ? r4o : r4e)];
+          mk[pm][i] = a1b[256 * pm + 16 * i + ((i & 1) ? r4o : r4e)];
       // delta1 (its operands: two 16-B reads per pixel tile)
       f32x4 av[2][2], d1[2];
 #pragma unroll
@@ -316,13 +302,8 @@ __global__ __launch_bounds__(256 * kD1cTeams, SRCNN_D1C_OCC) void d1c_grad12_ker
         __builtin_amdgcn_sched_barrier(0);
         const float bv = d1[k >> 2][k & 3];
         const float* x = xv[k % 3];
-        if (kD1cDiag & 4) {
 #pragma unroll
-          for (int m = 0; m < 5; m++) g1[m] = mfma::mma16(bv + m, bv, g1[m]);
-        } else {
-#pragma unroll
-          for (int m = 0; m < 5; m++) g1[m] = mfma::mma16(x[m], bv, g1[m]);
-        }
+        for (int m = 0; m < 5; m++) g1[m] = mfma::mma16(x[m], bv, g1[m]);
         gv = fmaf(x[5], bv, gv);
         gvb += bv;
         __builtin_amdgcn_sched_barrier(0);
@@ -367,9 +348,8 @@ __global__ __launch_bounds__(256 * kD1cTeams, SRCNN_D1C_OCC) void d1c_grad12_ker
   // Row 4 lg + i of tile m is the A-operand lane lq' = 4 lg + i, i.e. tap
   // (dy0 + lg, dx0 + i) for tiles 0-3.
   float* out = slab + (size_t)blockIdx.x * P12;
-  // (two teams: team 0 holds the sums; diagnostic 16: a runtime-false writer,
-  // so the accumulators stay live)
-  const bool writer = team == 0 && ((kD1cDiag & 16) ? g.batch < 0 : true);
+  // (two teams: team 0 holds the sums)
+  const bool writer = team == 0;
   if (writer)
 #pragma unroll
   for (int m = 0; m < 4; m++)

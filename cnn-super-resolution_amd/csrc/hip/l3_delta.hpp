@@ -23,48 +23,11 @@
 // the MFMA A operand and the per-channel row reads are at most 2-way bank
 // conflicted without padding.  The DMA realises the swizzle by choosing each
 // lane's global source quad.
-#ifdef SRCNN_L3_TIMING
-// diagnostics build only: per-block cycles spent between the phase barriers
-__device__ unsigned long long g_l3_timing[1024][4];
-#define SRCNN_L3_TICK(PH)                                             \
-  do {                                                                \
-    if (threadIdx.x == 0) {                                           \
-      const unsigned long long now_ = clock64();                      \
-      tacc[(PH + 3) & 3] += now_ - tlast;                             \
-      tlast = now_;                                                   \
-    }                                                                 \
-  } while (0)
-#else
-#define SRCNN_L3_TICK(PH) \
-  do {                    \
-  } while (0)
-#endif
-
-// diagnostics builds only (results invalid): drop one part of the delta2 phase
-#ifdef SRCNN_L3_DIAG_NOSTORE
-constexpr bool kL3DiagNoStore = true;
-#else
-constexpr bool kL3DiagNoStore = false;
-#endif
-#ifdef SRCNN_L3_DIAG_NOD2
-constexpr bool kL3DiagNoD2 = true;
-#else
-constexpr bool kL3DiagNoD2 = false;
-#endif
-#ifdef SRCNN_L3_DIAG_NOGW3
-constexpr bool kL3DiagNoGW3 = true;
-#else
-constexpr bool kL3DiagNoGW3 = false;
-#endif
-
 // Sample order: l3 walks the batch from the end.  l12 wrote the last
 // samples' A2 last, so they are the ones still in the MALL; and l3's own last
 // D2 rows are then the batch head, which d1 (grid-strided from the start)
 // reads first.
-#ifndef SRCNN_L3_REVERSE
-#define SRCNN_L3_REVERSE 1
-#endif
-__device__ __forceinline__ int l3_order(int s, int batch) { return SRCNN_L3_REVERSE ? batch - 1 - s : s; }
+__device__ __forceinline__ int l3_order(int s, int batch) { return batch - 1 - s; }
 
 struct L3Geom {
   int W, H;     // ground-truth sample (= network input size)
@@ -73,24 +36,11 @@ struct L3Geom {
   int batch;
 };
 
-#ifndef SRCNN_L3_THREADS
-#define SRCNN_L3_THREADS 512
-#endif
-constexpr int kL3Threads = SRCNN_L3_THREADS;
+// (768 / 1024 threads per block measured slower: the three barrier-separated
+// phases, not occupancy, set the pace)
+constexpr int kL3Threads = 512;
 constexpr int kL3TPF = (1024 + kL3Threads - 1) / kL3Threads;  // L3 outputs per thread (w3 * h3 <= 1024)
-// diagnostics builds: store delta2 from the delta2 phase instead of holding it
-// in registers until the next sample's Q phase
-#ifdef SRCNN_L3_DIRECT_D2
-constexpr bool kL3DirectD2 = true;
-#else
-constexpr bool kL3DirectD2 = false;
-#endif
 constexpr int kL3MaxOut = kL3TPF * kL3Threads;
-// units per wave whose masked delta2 is held for the next sample's Q phase
-// (the others are stored straight from the delta2 phase); default: all
-#ifndef SRCNN_L3_DEFER
-#define SRCNN_L3_DEFER 99
-#endif
 
 // float index of A2[p][n] in the swizzled LDS image
 template <int N2>
@@ -254,13 +204,13 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
 
   // masked delta2 of this wave's units (slot j = unit wave + 8j), held
   // until the next sample's Q phase; D2 rows past the sample are not stored
-  f32x4 d2k[kL3DirectD2 ? 1 : kUMax][NT];
+  f32x4 d2k[kUMax][NT];
   float* d2dst = D2;
   bool d2pend = false;
 #define SRCNN_L3_D2_STORE(J)                                                           \
   do {                                                                                 \
     const int q_ = 16 * (wave + nwaves * (J)) + lq;                                    \
-    if (d2pend && q_ < npx2 && !kL3DiagNoStore) {                                      \
+    if (d2pend && q_ < npx2) {                                      \
       float* dst_ = d2dst + (size_t)q_ * N2 + 4 * lg;                                  \
       _Pragma("unroll") for (int t = 0; t < NT; t++)                                   \
         if (kNtMask & 2)                                                               \
@@ -275,16 +225,12 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
     SRCNN_L3_A2_DMA(l3_order(blockIdx.x, g.batch), smem);
     SRCNN_L3_T_PREFETCH(l3_order(blockIdx.x, g.batch));
   }
-#ifdef SRCNN_L3_TIMING
-  unsigned long long tacc[4] = {0, 0, 0, 0}, tlast = clock64();
-#endif
 
   for (int sample = blockIdx.x; sample < g.batch; sample += gridDim.x) {
     // this sample's A2 DMA has landed in every wave; the previous sample's
     // readers of both regions and of d3g are done
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    SRCNN_L3_TICK(0);
     const float* a2s = smem + cur * L.region;
     float* other = smem + (cur ^ 1) * L.region;
     float* qs = other;  // [npx2][K3]
@@ -313,7 +259,7 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
         for (int s = 0; s < KQ; s++)
 #pragma unroll
           for (int t = 0; t < TT; t++) acc[t] = mfma::mma16(av[s], wq[s][t], acc[t]);
-        if (!kL3DirectD2 && j < SRCNN_L3_DEFER) SRCNN_L3_D2_STORE(j);
+        SRCNN_L3_D2_STORE(j);
         // Q[u0 + 4lg + i][tap = 16t + lq] (the region holds whole units: rows
         // past the sample are written too, never read)
 #pragma unroll
@@ -329,7 +275,6 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
     }
     d2pend = false;
     __syncthreads();
-    SRCNN_L3_TICK(1);
 
     // ---- L3 = B3 + diagonal sums of Q; last delta; squared error ----
 #pragma unroll
@@ -354,14 +299,11 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
       }
     }
     __syncthreads();
-    SRCNN_L3_TICK(2);
 
     // Q is consumed: the next sample's A2 streams into its region meanwhile
     // (Measured slower: loading the next A2 into registers under the Q MFMAs
     // and writing it here, so its HBM reads leave the delta2 phase.)
-#ifndef SRCNN_L3_DIAG_NODMA
     if (has_next) SRCNN_L3_A2_DMA(l3_order(sample + gridDim.x, g.batch), other);
-#endif
 
     // ---- per 16-pixel unit: delta2 and gW3 MFMAs ----
     //   delta2[q][n] = [A2 > 0] * sum_tap delta3(q - off(tap)) W3[tap][n]
@@ -404,52 +346,33 @@ __global__ __launch_bounds__(kL3Threads, 1) void l3_delta_kernel(
         for (int s = 0; s < KT; s++)
 #pragma unroll
           for (int t = 0; t < NT; t++)
-            if (!kL3DiagNoD2) acc[t] = mfma::mma16(wd[s][t], ad[s], acc[t]);
+            acc[t] = mfma::mma16(wd[s][t], ad[s], acc[t]);
 #pragma unroll
-        for (int s = 0; s < 4 * !kL3DiagNoGW3; s++)
+        for (int s = 0; s < 4; s++)
 #pragma unroll
           for (int t3 = 0; t3 < TT; t3++)
 #pragma unroll
             for (int t = 0; t < NT; t++)
               gacc[t3][t] = mfma::mma16(ag[s][t3], bg[s][t], gacc[t3][t]);
-        if (kL3DirectD2 || j >= SRCNN_L3_DEFER) {
-          const int q_ = u0 + lq;
-          if (q_ < npx2 && !kL3DiagNoStore) {
-            float* dst_ = D2 + ((size_t)l3_order(sample, g.batch) * npx2 + q_) * N2 + 4 * lg;
+        // held for the next sample's Q phase (stored from the delta2 phase,
+        // or only some units deferred: slower)
 #pragma unroll
-            for (int t = 0; t < NT; t++) {
-              f32x4 v;
+        for (int t = 0; t < NT; t++)
 #pragma unroll
-              for (int i = 0; i < 4; i++) v[i] = mk[t][i] > 0.0f ? acc[t][i] : 0.0f;
-              *reinterpret_cast<f32x4*>(dst_ + 16 * t) = v;
-            }
-          }
-        } else {
-#pragma unroll
-          for (int t = 0; t < NT; t++)
-#pragma unroll
-            for (int i = 0; i < 4; i++) d2k[j][t][i] = mk[t][i] > 0.0f ? acc[t][i] : 0.0f;
-        }
+          for (int i = 0; i < 4; i++) d2k[j][t][i] = mk[t][i] > 0.0f ? acc[t][i] : 0.0f;
       }
     }
     d2dst = D2 + (size_t)l3_order(sample, g.batch) * npx2 * N2;
     d2pend = true;
-    SRCNN_L3_TICK(3);
     cur ^= 1;
   }
-  if (!kL3DirectD2)
 #pragma unroll
-    for (int j = 0; j < kUMax; j++)
-      if (j < SRCNN_L3_DEFER) SRCNN_L3_D2_STORE(j);
+  for (int j = 0; j < kUMax; j++) SRCNN_L3_D2_STORE(j);
 #undef SRCNN_L3_D2_STORE
 #undef SRCNN_L3_A2_DMA
   SRCNN_CLOCK_END(g_clk, 1);
 #undef SRCNN_L3_T_PREFETCH
 
-#ifdef SRCNN_L3_TIMING
-  if (threadIdx.x == 0)
-    for (int k = 0; k < 4; k++) g_l3_timing[blockIdx.x][k] = tacc[k];
-#endif
   // ---- block reduction of the partial gradients, waves in order ----
   __syncthreads();
   for (int w = 0; w < nwaves; w++) {

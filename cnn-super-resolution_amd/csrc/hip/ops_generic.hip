@@ -309,6 +309,7 @@ __global__ void lazy_update_kernel(fused::LazyUpdate u) {
 
 int lazy_update(const fused::LazyUpdate& u, hipStream_t s) {
   SRCNN_PROFILE("update_all", s);
+  kernels_note("lazy_update");
   hipLaunchKernelGGL(lazy_update_kernel, dim3(grid_for(u.off[6], 256, 2048)), dim3(256), 0, s, u);
   SRCNN_LAUNCH_TRY();
   return SRCNN_OK;

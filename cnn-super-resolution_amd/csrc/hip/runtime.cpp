@@ -37,6 +37,16 @@ int fail(int code, const char* fmt, ...) {
 
 void clear_error() { t_last_error.clear(); }
 
+// kernels launched by this thread's most recent network-level call
+// (srcnn_last_kernels)
+static thread_local std::string t_kernels;
+void kernels_reset() { t_kernels.clear(); }
+void kernels_note(const char* name) {
+  if (!t_kernels.empty()) t_kernels += ',';
+  t_kernels += name;
+}
+const char* kernels_last() { return t_kernels.c_str(); }
+
 const char* last_error() { return t_last_error.c_str(); }
 
 namespace prof {

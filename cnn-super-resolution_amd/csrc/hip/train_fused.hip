@@ -47,10 +47,7 @@ constexpr int kXsMax = 1536;  // input sample / region tile (floats) staged in L
 // (row * kL12S + col) mod 32 (ds_read_b32 banks 32 lanes at a time), which
 // is (pixel index + const) mod 32 -- 32 distinct banks -- when kL12S == ow
 // (mod 32): 57 = 25 + 32 makes the default 33x33 tile (ow 25) conflict-free.
-#ifndef SRCNN_L12_S
-#define SRCNN_L12_S 57
-#endif
-constexpr int kL12S = SRCNN_L12_S;
+constexpr int kL12S = 57;
 constexpr int kL12Rows = 40;
 constexpr int kL12Tile = kL12S * (kL12Rows + 1);  // + a zero row read by the padded tap
 constexpr int kL12Regs = (kXsMax + 255) / 256;    // register-staged X tile (w * h <= kXsMax)
@@ -76,50 +73,27 @@ struct Geom {
 // held-clock probe slots (common.hpp): 0 l12_fwd, 1 l3_delta, 2 d1_grad12
 __device__ unsigned long long g_clk[3][kClockBlocks][2];
 
-#ifndef SRCNN_L12_GRID
-#define SRCNN_L12_GRID 512  // grid cap (blocks) = 256 CUs x 2 resident blocks: the samples are
-                            // written in index order, which l3 reads back in reverse (MALL)
-#endif
 // streaming-cache hints (bits): 1 l3 A2 DMA nt, 2 l3 D2 stores nt, 4 d1
 // operand DMA nt, 8 l12 A1 stores nt.  Default 1 | 8 (same-box A/B, steady
 // state, 2 reps: step 0.938 -> 0.931 ms): A1 (655 MB per step, read back only
 // by d1) streams past the caches, so more of the A2 that l12 writes just
 // before l3 reads it stays in the 256 MB MALL (l3 -4.5%); nt on the D2
 // stores or the d1 DMA was slower.
-#ifndef SRCNN_NT
-#define SRCNN_NT 9
-#endif
-constexpr int kNtMask = SRCNN_NT;
-#ifndef SRCNN_L12_PD
-#define SRCNN_L12_PD 4  // L1 X-gather prefetch distance (k-steps); 0 = compiler schedule
-#endif
-constexpr int kL12PD = SRCNN_L12_PD;
-// diagnostics builds only (results invalid): 1 drop the A1 stores, 2 the A2 stores
-// (and with them the L2 MFMAs, dead code then), 4 the A2 stores behind a
-// runtime-false test (the L2 MFMAs stay)
-#ifdef SRCNN_L12_DIAG
-constexpr int kL12Diag = SRCNN_L12_DIAG;
-#else
-constexpr int kL12Diag = 0;
-#endif
-#ifndef SRCNN_L3R_GRID
-#define SRCNN_L3R_GRID 512  // l3r grid cap: 256 CUs x 2 resident blocks
-#endif
-// 1: A2 leaves l12 as whole 128-B pixel rows: at each chunk end the wave
-// regroups its A2 tile through a 4.6 KB LDS scratch into row order (one write
-// and one read per quad, a single LDS round trip per chunk), and the stores
-// inside the next chunk's MFMA stream write 1 KB contiguous each.  As held
-// (0), each store wrote 32 rows x 32 B; those stores cost 6% of l12
-// (SRCNN_L12_DIAG=4).  Same-box A/B (profiles/r04_ab_a2rows): l12 0.3068 ->
-// 0.3049 ms, l3 0.1559 -> 0.1547 ms, step 0.8668 -> 0.8641 ms at batch 4096;
-// the 512-tile shard unchanged (l12 +0.4 us)
-#ifndef SRCNN_L12_A2ROWS
-#define SRCNN_L12_A2ROWS 1
-#endif
+constexpr int kNtMask = 9;
+// L1 X-gather prefetch distance (k-steps), pinned by sched barriers
+constexpr int kL12PD = 4;
+// grid caps (blocks): 256 CUs x 2 resident blocks.  l12 writes the samples
+// in index order, which l3 reads back in reverse (MALL)
+constexpr int kL12Grid = 512, kL3RGrid = 512;
+// A2 leaves l12 as whole 128-B pixel rows (n2 = 32): at each chunk end the
+// wave regroups its A2 tile through a 4.6 KB LDS scratch into row order (one
+// write and one read per quad, a single LDS round trip per chunk), and the
+// stores inside the next chunk's MFMA stream write 1 KB contiguous each.  As
+// held, each store wrote 32 rows x 32 B; those stores cost 6% of l12
+// (round-4 diagnostic build).  Same-box A/B (profiles/r04_ab_a2rows): l12
+// 0.3068 -> 0.3049 ms, l3 0.1559 -> 0.1547 ms, step 0.8668 -> 0.8641 ms at
+// batch 4096; the 512-tile shard unchanged (l12 +0.4 us)
 constexpr int kL12A2S = 36;  // A2 scratch row stride (floats)
-#ifndef SRCNN_L12_WAVES
-#define SRCNN_L12_WAVES 2  // minimum waves per SIMD (register budget 512 / this)
-#endif
 // kLazy (srcnn_train_fwd_bwd_lazy): the previous data-parallel step's SGD
 // update rides in the prologue.  Every block forms the updated W1 / B1 / W2 /
 // B2 it needs in registers from lz's (P, M, G) -- the same sgd_step as
@@ -128,7 +102,7 @@ constexpr int kL12A2S = 36;  // A2 scratch row stride (floats)
 // lz.Mo, which l3 and d1 read after this kernel.  No update launch between
 // the gradient all-reduce and the next step.
 template <int N1, int N2, int F1, bool kLazy = false>
-__global__ __launch_bounds__(256, SRCNN_L12_WAVES) void l12_fwd_kernel(
+__global__ __launch_bounds__(256, 2) void l12_fwd_kernel(
     const float* __restrict__ X, const float* __restrict__ W1, const float* __restrict__ B1,
     const float* __restrict__ W2, const float* __restrict__ B2, float* __restrict__ A1,
     float* __restrict__ A2, Geom g, LazyUpdate lz) {
@@ -136,7 +110,7 @@ __global__ __launch_bounds__(256, SRCNN_L12_WAVES) void l12_fwd_kernel(
   static_assert(N2 <= 32 && N2 % 8 == 0 && K1 % 2 == 1 && N1 % 32 == 0,
                 "transposed l12: one 32-row L2 tile, odd tap count");
   __shared__ float xs[kL12Tile];  // X tile at the fixed row stride kL12S (+ zero rows)
-  constexpr bool kA2Rows = SRCNN_L12_A2ROWS && N2 == 32;  // (a row = 8 quads)
+  constexpr bool kA2Rows = N2 == 32;  // (a row = 8 quads)
   __shared__ __attribute__((aligned(16))) float a2sc[kA2Rows ? 4 * 32 * kL12A2S : 4];
   // L2 bias as the accumulator's initial value: register r of half h is
   // channel crow(r, h) (one 16x32 image, read as 4 broadcast 16-B loads)
@@ -148,18 +122,51 @@ __global__ __launch_bounds__(256, SRCNN_L12_WAVES) void l12_fwd_kernel(
   const int h = lane >> 5, li = lane & 31;
   const int npx = g.ow * g.oh;
   const int nch = (npx + 31) / 32;
+  // The next sample's X tile is register-staged during the current sample
+  // (its loads retire under the MFMAs instead of stalling both barriers);
+  // the LDS copy uses a fixed row stride so every L1 B operand is a per-half
+  // base + immediate (tap 2s+1 sits 1 or kL12S - F1 + 1 floats past tap 2s).
+  for (int i = threadIdx.x; i < kL12Tile; i += blockDim.x) xs[i] = 0.0f;
+  const int xn = g.W * g.H;
+  float xr[kL12Regs];
+  auto xload = [&](int smp) {
+    const float* src = X + (size_t)smp * xn;
+#pragma unroll
+    for (int k = 0; k < kL12Regs; k++) {
+      const int i = threadIdx.x + 256 * k;
+      xr[k] = i < xn ? src[i] : 0.0f;
+    }
+  };
+  // (issued first: its loads are in flight under the parameter loads)
+  if ((int)blockIdx.x < g.batch) xload(blockIdx.x);
   // kLazy: the updated W1 | B1 | W2 | B2 (the flat buffer's first P12
   // floats) are formed once per block into LDS, each by one thread with
   // coalesced loads; the register operands below are read from there
   constexpr int P12 = F1 * F1 * N1 + N1 + N1 * N2 + N2;
   __shared__ float lzs[kLazy ? P12 : 1];
   if constexpr (kLazy) {
+    // every load of the thread in flight at once (a rolled loop waited out
+    // one L2 round trip per element: l12 +9 us at one sample per block)
+    constexpr int kIt = (P12 + 255) / 256;
+    float lw[kIt], lm[kIt], lgr[kIt];
+#pragma unroll
+    for (int k = 0; k < kIt; k++) {
+      const int i = threadIdx.x + 256 * k;
+      if (i < P12) {
+        lw[k] = lz.P[i];
+        lm[k] = lz.M[i];
+        lgr[k] = lz.G[i];
+      }
+    }
     lazy_write_slice(lz);
-    for (int i = threadIdx.x; i < P12; i += blockDim.x) {
-      const int seg = param_seg(lz.off, i);
-      float w_ = lz.P[i], m_ = lz.M[i];
-      sgd_step(w_, m_, seg, lz.G[i], lz.lr[seg >> 1], lz.mu, lz.wd, lz.batch);
-      lzs[i] = w_;
+#pragma unroll
+    for (int k = 0; k < kIt; k++) {
+      const int i = threadIdx.x + 256 * k;
+      if (i < P12) {
+        const int seg = param_seg(lz.off, i);
+        sgd_step(lw[k], lm[k], seg, lgr[k], lz.lr[seg >> 1], lz.mu, lz.wd, lz.batch);
+        lzs[i] = lw[k];
+      }
     }
     __syncthreads();
   }
@@ -191,22 +198,6 @@ __global__ __launch_bounds__(256, SRCNN_L12_WAVES) void l12_fwd_kernel(
     b2i[threadIdx.x >> 4][threadIdx.x & 15] = c_ < N2 ? prm(3, c_) : 0.0f;
   }
 
-  // The next sample's X tile is register-staged during the current sample
-  // (its loads retire under the MFMAs instead of stalling both barriers);
-  // the LDS copy uses a fixed row stride so every L1 B operand is a per-half
-  // base + immediate (tap 2s+1 sits 1 or kL12S - F1 + 1 floats past tap 2s).
-  for (int i = threadIdx.x; i < kL12Tile; i += blockDim.x) xs[i] = 0.0f;
-  const int xn = g.W * g.H;
-  float xr[kL12Regs];
-  auto xload = [&](int smp) {
-    const float* src = X + (size_t)smp * xn;
-#pragma unroll
-    for (int k = 0; k < kL12Regs; k++) {
-      const int i = threadIdx.x + 256 * k;
-      xr[k] = i < xn ? src[i] : 0.0f;
-    }
-  };
-  if ((int)blockIdx.x < g.batch) xload(blockIdx.x);
   for (int sample = blockIdx.x; sample < g.batch; sample += gridDim.x) {
     __syncthreads();  // previous sample's readers are done with xs
 #pragma unroll
@@ -235,7 +226,7 @@ __global__ __launch_bounds__(256, SRCNN_L12_WAVES) void l12_fwd_kernel(
     int pc0 = 0;  // kA2Rows: the pending chunk's first pixel
     auto store_prev = [&](int k) {  // store k of the pending chunk (exec-masked)
       if (pok) {
-        if (k < 4 * NT1 && !(kL12Diag & 1)) {
+        if (k < 4 * NT1) {
           // blocked A1 (internal to the fused step, read only by d1): block k
           // of a chunk is 64 lanes x 16 B in lane order, one contiguous 1-KB
           // store; lanes past the sample store their clamped pixel's copy
@@ -249,7 +240,7 @@ __global__ __launch_bounds__(256, SRCNN_L12_WAVES) void l12_fwd_kernel(
             *reinterpret_cast<float4*>(pa1p + 256 * k) =
                 make_float4(pa1[t][4 * q], pa1[t][4 * q + 1], pa1[t][4 * q + 2], pa1[t][4 * q + 3]);
           }
-        } else if (kA2Rows && k >= 4 * NT1 && !(kL12Diag & 2) && (!(kL12Diag & 4) || g.batch < 0)) {
+        } else if (kA2Rows && k >= 4 * NT1) {
           // row store q: pixels 8q .. 8q + 7 of the chunk, lane L -> pixel
           // 8q + L / 8, quad L % 8 (already relu'd, in pa2's quad q)
           const int q = k - 4 * NT1;
@@ -259,7 +250,7 @@ __global__ __launch_bounds__(256, SRCNN_L12_WAVES) void l12_fwd_kernel(
             for (int e = 0; e < 4; e++) v_[e] = pa2[4 * q + e];
             *reinterpret_cast<f32x4*>(pa2p + (8 * q + (lane >> 3)) * N2 + 4 * (lane & 7)) = v_;
           }
-        } else if (!kA2Rows && k >= 4 * NT1 && pval && !(kL12Diag & 2) && (!(kL12Diag & 4) || g.batch < 0)) {
+        } else if (!kA2Rows && k >= 4 * NT1 && pval) {
           const int q = k - 4 * NT1;
           *reinterpret_cast<float4*>(pa2p + 8 * q) =
               make_float4(fmaxf(pa2[4 * q], 0.0f), fmaxf(pa2[4 * q + 1], 0.0f),
@@ -357,23 +348,6 @@ __global__ __launch_bounds__(256, SRCNN_L12_WAVES) void l12_fwd_kernel(
 #include "l3_delta.hpp"
 #include "l3r.hpp"
 
-#ifdef SRCNN_D1_TIMING
-// diagnostics build only: wave 0's cycles per section of the chunk loop
-// [block][wave][section]; [6], [7]: s_memtime / s_memrealtime (100 MHz) deltas
-// over the block, whose ratio is the shader clock the chip held
-__device__ unsigned long long g_d1_timing[1024][4][8];
-#define SRCNN_D1_TICK(PH)                           \
-  do {                                              \
-    const unsigned long long now_ = clock64();      \
-    tacc[(PH + 5) % 6] += now_ - tlast;             \
-    tlast = now_;                                   \
-  } while (0)
-#else
-#define SRCNN_D1_TICK(PH) \
-  do {                    \
-  } while (0)
-#endif
-
 // ---------------------------------------------------------------------------
 // Kernel 3: delta1 + gW2/gB2 + gW1/gB1
 //
@@ -391,32 +365,9 @@ __device__ unsigned long long g_d1_timing[1024][4][8];
 // With f1 = 9 that is 80 MFMA taps + 1 VALU tap, where a 32-row tap tiling
 // issues 96 rows (81 taps + ones row + 14 pad): 1/6 fewer gW1 MFMA cycles.
 // ---------------------------------------------------------------------------
-// diagnostics builds only (results invalid): drop one part of the d1 chunk
-#ifdef SRCNN_D1_DIAG
-constexpr int kD1Diag = SRCNN_D1_DIAG;
-#else
-constexpr int kD1Diag = 0;
-#endif
-constexpr bool kD1DiagNoD1 = kD1Diag & 1, kD1DiagNoGW2 = kD1Diag & 2, kD1DiagNoMask = kD1Diag & 4,
-               kD1DiagNoGW1 = kD1Diag & 8, kD1DiagNoDma = kD1Diag & 16,
-               // 32: gW1 X gathers at lane-linear (bank-conflict-free) addresses;
-               // 64: delta1 operand reads at lane-linear addresses
-               kD1DiagLinX = kD1Diag & 32, kD1DiagLinD1 = kD1Diag & 64;
-#ifndef SRCNN_D1_D2SW
-#define SRCNN_D1_D2SW 1
-#endif
-constexpr bool kD1D2Sw = SRCNN_D1_D2SW;
-#ifndef SRCNN_D1_A1SW
-#define SRCNN_D1_A1SW 1
-#endif
-constexpr bool kD1A1Sw = SRCNN_D1_A1SW;
-#ifndef SRCNN_D1_TOPWAIT
-#define SRCNN_D1_TOPWAIT 1  // sample top waits for the X tile only, not the next chunk's operands
-#endif
-constexpr bool kD1TopWait = SRCNN_D1_TOPWAIT;
-#ifndef SRCNN_D1_DMA_STEPS
-#define SRCNN_D1_DMA_STEPS 8  // gW1 k-steps the next work item's operand DMA is spread over
-#endif
+// gW1 k-steps the next work item's operand DMA is spread over (1, 2 or 4
+// measured 0.4-0.7% slower)
+constexpr int kD1DmaSteps = 8;
 template <int N1, int N2, int F1>
 __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
     const float* __restrict__ X, const float* __restrict__ A1, const float* __restrict__ D2,
@@ -430,20 +381,19 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
   constexpr int MT = K1 / 16;             // 16-tap MFMA tiles
   constexpr int KR = K1 - 16 * MT;        // taps left to the VALU
   constexpr int KD = N2 / 4;              // delta1 k-steps (over n)
-  // delta2 LDS image rows: SRCNN_D1_D2SW = 1: N2 floats, quads of row r
-  // XOR-swizzled by d2sw(r) = (r >> 1) mod N2/4; 0: one pad quad per row
-  constexpr int DS = kD1D2Sw ? N2 : N2 + 4;
+  // delta2 LDS image rows: N2 floats, quads of row r XOR-swizzled by
+  // d2sw(r) = (r >> 1) mod N2/4 (a padded image cost one DMA per chunk more)
+  constexpr int DS = N2;
   constexpr int WS = N2 + 1;              // W2 image (N1 * N2 floats) within N1 * WS
   constexpr int NW1 = K1 * N1, NW2 = N1 * N2;
   constexpr int P12 = NW1 + N1 + NW2 + N2;  // [gW1 | gB1 | gW2 | gB2]
   static_assert(N2 % 4 == 0 && N1 % 32 == 0 && KR <= 4, "d1 tile shape");
   constexpr int RED1 = MT * NQ * 4 * 64, RED2 = NT1 * NT2 * 16 * 64, REDV = (KR + 1) * NQ * 64;
   constexpr int RED = RED1 + RED2 + REDV;
-  // A1 LDS image rows: SRCNN_D1_A1SW = 1: N1 floats with the 16-B quads of
-  // row r XOR-swizzled by a1sw(r) (8 * bit 2 + 4 * bit 3 of r); 0: rows
-  // padded by one quad.  Both make the gW2 and mask reads conflict-free;
-  // the swizzle saves one DMA instruction per chunk.
-  constexpr int A1P = kD1A1Sw ? N1 : N1 + 4;
+  // A1 LDS image rows: N1 floats with the 16-B quads of row r XOR-swizzled
+  // by a1sw(r) (8 * bit 2 + 4 * bit 3 of r): the gW2 and mask reads are
+  // conflict-free, one DMA instruction per chunk fewer than padded rows
+  constexpr int A1P = N1;
   constexpr int A1K = (32 * A1P + 255) / 256;  // 16-byte DMA instructions per A1 chunk
   constexpr int A1S = 256 * A1K;               // per-wave A1 staging
   constexpr int D2S = 32 * DS;                 // per-wave delta2 chunk image [32][DS]
@@ -522,13 +472,12 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
     const int rmax_ = npx - 1 - (C) * 32;                                         \
     const size_t px0_ = (size_t)(SMP) * npx + (size_t)(C) * 32;                   \
     if ((K) < A1K) {                                                              \
-      /* image quad f = row r, slot q of the [32][A1P] image (padded: the pad */ \
-      /* re-reads quad 0; swizzled: slot q holds quad q ^ a1sw(r)); in the */    \
-      /* blocked chunk, quad j of pixel r is lane r + 32(j & 1) of block */      \
-      /* j >> 1: 64-B runs of 4 pixels per half-block */                         \
+      /* image quad f = row r, slot q of the [32][A1P] image (slot q holds */   \
+      /* quad q ^ a1sw(r)); in the blocked chunk, quad j of pixel r is lane */   \
+      /* r + 32(j & 1) of block j >> 1: 64-B runs of 4 pixels per half-block */  \
       const uint32_t f_ = (K) * 64 + (uint32_t)l_;                                \
       const uint32_t r_ = f_ / (A1P / 4), j0_ = f_ - r_ * (A1P / 4);              \
-      const uint32_t j_ = kD1A1Sw ? (j0_ ^ (uint32_t)a1sw(r_)) : (j0_ < N1 / 4 ? j0_ : 0u); \
+      const uint32_t j_ = j0_ ^ (uint32_t)a1sw(r_);                              \
       const uint32_t off_ = (j_ >> 1) * 256 + 4 * (min(r_, 31u) + 32 * (j_ & 1u)); \
       __builtin_amdgcn_global_load_lds(                                           \
           (const void*)(A1 + ((size_t)(SMP) * nch + (C)) * (32 * N1) + off_),     \
@@ -536,11 +485,10 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
           (kNtMask & 4) ? 2 : 0);                                                 \
     } else {                                                                      \
       /* delta2 rows, 16 B / lane: slot quad Q of the [32][DS] image is row */   \
-      /* Q / (DS/4), slot Q % (DS/4) (swizzled: quad slot ^ d2sw(row); */        \
-      /* padded: the pad quad re-reads quad 0) */                                \
+      /* Q / (DS/4), slot Q % (DS/4) holding quad slot ^ d2sw(row) */            \
       const uint32_t q_ = 64 * ((K) - A1K) + (uint32_t)l_;                        \
       const uint32_t r_ = q_ / (DS / 4), j0_ = q_ - r_ * (DS / 4);                \
-      const uint32_t j_ = kD1D2Sw ? (j0_ ^ (uint32_t)d2sw(r_)) : j0_;             \
+      const uint32_t j_ = j0_ ^ (uint32_t)d2sw(r_);                               \
       const uint32_t off_ = (uint32_t)min((int)r_, rmax_) * N2 + (j_ < N2 / 4 ? 4 * j_ : 0u); \
       __builtin_amdgcn_global_load_lds(                                           \
           (const void*)(D2 + px0_ * N2 + off_),                                   \
@@ -554,10 +502,6 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
   } while (0)
   const int nch = (npx + 31) / 32;
 
-#ifdef SRCNN_D1_TIMING
-  unsigned long long tacc[6] = {0, 0, 0, 0, 0, 0}, tlast = clock64();
-  const unsigned long long c0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
-#endif
   // X tile of a sample -> xs buffer by 4-byte LDS-DMA (lane-linear)
   const int xn = g.W * g.H, xk = (xn + 63) / 64;
 #define SRCNN_D1_X_DMA(SMP, DST)                                                  \
@@ -589,15 +533,14 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
     // (__syncthreads() would add its own vmcnt(0): a bare s_barrier after
     // explicit waits; lgkmcnt(0) retires this wave's X reads of the buffer
     // the others are about to refill)
-    if (!kD1TopWait || wave >= nch) {
+    if (wave >= nch) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     } else {
-      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(kD1TopWait ? kDmaK : 0) : "memory");
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(kDmaK) : "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
     }
-    SRCNN_D1_TICK(4);
     const float* xs = xsb + xbuf * kXsMax;
     const int next = sample + (int)gridDim.x;
     const bool has_next = next < g.batch;
@@ -605,7 +548,6 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
 
     for (int c = wave; c < nch; c += 4) {
       // this chunk's operand DMA has landed
-      SRCNN_D1_TICK(0);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_wave_barrier();
       if (c == wave && has_next) SRCNN_D1_X_DMA(next, xsb + (xbuf ^ 1) * kXsMax);
@@ -615,7 +557,6 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
         for (int i = (npx - c * 32) * DS + l_; i < D2S; i += 64) d2me[i] = 0.0f;
       }
 
-      SRCNN_D1_TICK(1);
       // delta1[p][c] = sum_n delta2[p][n] * W2[c][n]  (layer_deltas.cl, f=1)
       f32x4 d1[2][NQ];
 #pragma unroll
@@ -629,12 +570,10 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
       asm volatile("" : "+v"(dab));
 #pragma unroll
       for (int s = 0; s < KD; s++) {
-        const int n = 4 * s + lg;
         float a[2], b[NQ];
 #pragma unroll
         for (int pm = 0; pm < 2; pm++)
-          a[pm] = kD1DiagLinD1 ? d2me[lane + 64 * ((s + pm) & 7)]
-                               : d2me[kD1D2Sw ? (dab ^ (4 * s)) + 16 * pm * DS : (16 * pm + lq) * DS + n];
+          a[pm] = d2me[(dab ^ (4 * s)) + 16 * pm * DS];
         if constexpr (NQ == 4) {
           const f32x4 bv = *reinterpret_cast<const f32x4*>(w2s + (s * 64 + lane) * NQ);
 #pragma unroll
@@ -647,9 +586,8 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
         for (int pm = 0; pm < 2; pm++)
 #pragma unroll
           for (int t = 0; t < NQ; t++)
-            if (!kD1DiagNoD1) d1[pm][t] = mfma::mma16(a[pm], b[t], d1[pm][t]);
+            d1[pm][t] = mfma::mma16(a[pm], b[t], d1[pm][t]);
       }
-      SRCNN_D1_TICK(2);
       // gW2[c][n] += sum_p A1[p][c] delta2[p][n]; gB2[n] += sum_p delta2[p][n]
       // swizzled image: pixel crow(s, h), channel 32t + li sits at
       // gw2b[t][bit 2 of s] + ((s & 3) + 8 (s >> 2)) A1P (crow's bit 2 is h)
@@ -668,19 +606,15 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
       }
 #pragma unroll
       for (int s = 0; s < 16; s++) {
-        const int pr = crow(s, h);
 #pragma unroll
         for (int u = 0; u < NT2; u++) {
           const int n = 32 * u + li;
           const int pr0 = (s & 3) + 8 * (s >> 2);  // crow(s, 0); pr = pr0 + 4h
-          const float b = n < N2 ? d2me[kD1D2Sw ? (gdb ^ (4 * d2sw(pr0))) + pr0 * DS : pr * DS + n] : 0.0f;
+          const float b = n < N2 ? d2me[(gdb ^ (4 * d2sw(pr0))) + pr0 * DS] : 0.0f;
           gb2[u] += b;
 #pragma unroll
           for (int t = 0; t < NT1; t++)
-            if (!kD1DiagNoGW2)
-              g2[t][u] = mma(a1me[kD1A1Sw ? gw2b[t][(s >> 2) & 1] + ((s & 3) + 8 * (s >> 2)) * A1P
-                                          : pr * A1P + 32 * t + li],
-                             b, g2[t][u]);
+            g2[t][u] = mma(a1me[gw2b[t][(s >> 2) & 1] + ((s & 3) + 8 * (s >> 2)) * A1P], b, g2[t][u]);
         }
       }
 
@@ -696,13 +630,8 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
         for (int t = 0; t < NQ; t++)
 #pragma unroll
           for (int i = 0; i < 4; i++)
-            if (!kD1DiagNoMask)
-              d1[pm][t][i] = a1me[kD1A1Sw ? (mskb ^ (16 * t)) + (16 * pm + i) * A1P
-                                          : (16 * pm + 4 * lg + i) * A1P + 16 * t + lq] > 0.0f
-                                 ? d1[pm][t][i]
-                                 : 0.0f;
+            d1[pm][t][i] = a1me[(mskb ^ (16 * t)) + (16 * pm + i) * A1P] > 0.0f ? d1[pm][t][i] : 0.0f;
 
-      SRCNN_D1_TICK(3);
       // next chunk's operand DMA overlaps the gW1 MFMAs (the images' reads retired)
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
@@ -724,12 +653,12 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
     const int y_ = (int)(((float)q_ + 0.5f) * inv_ow);                              \
     return q_ + y_ * (g.W - g.ow);                                                  \
   }())
-        constexpr int kDmaPerStep = (kDmaK + SRCNN_D1_DMA_STEPS - 1) / SRCNN_D1_DMA_STEPS;
+        constexpr int kDmaPerStep = (kDmaK + kD1DmaSteps - 1) / kD1DmaSteps;
         float acur[MT], rcur[KR > 0 ? KR : 1];
         {
           const int xb = SRCNN_D1_XB(0);
 #pragma unroll
-          for (int m = 0; m < MT; m++) acur[m] = kD1DiagLinX ? xs[(lane + 64 * m + xb) & 1023] : xs[xb + toff[m]];
+          for (int m = 0; m < MT; m++) acur[m] = xs[xb + toff[m]];
 #pragma unroll
           for (int r = 0; r < KR; r++) {
             const int tap = 16 * MT + r;
@@ -743,7 +672,7 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
           if (s + 1 < 8) {
             const int xb = SRCNN_D1_XB(s + 1);
 #pragma unroll
-            for (int m = 0; m < MT; m++) anxt[m] = kD1DiagLinX ? xs[(lane + 64 * m + xb) & 1023] : xs[xb + toff[m]];
+            for (int m = 0; m < MT; m++) anxt[m] = xs[xb + toff[m]];
 #pragma unroll
             for (int r = 0; r < KR; r++) {
               const int tap = 16 * MT + r;
@@ -754,7 +683,7 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
           for (int m = 0; m < MT; m++)
 #pragma unroll
             for (int t = 0; t < NQ; t++)
-              if (!kD1DiagNoGW1) g1[m][t] = mfma::mma16(acur[m], d1[pm][t][i], g1[m][t]);
+              g1[m][t] = mfma::mma16(acur[m], d1[pm][t][i], g1[m][t]);
 #pragma unroll
           for (int t = 0; t < NQ; t++) {
 #pragma unroll
@@ -763,7 +692,7 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
           }
 #pragma unroll
           for (int k = 0; k < kDmaPerStep; k++)
-            if (kDmaPerStep * s + k < kDmaK && !kD1DiagNoDma) SRCNN_D1_DMA_K(dsmp, dch, kDmaPerStep * s + k);
+            if (kDmaPerStep * s + k < kDmaK) SRCNN_D1_DMA_K(dsmp, dch, kDmaPerStep * s + k);
           if (s + 1 < 8) {
 #pragma unroll
             for (int m = 0; m < MT; m++) acur[m] = anxt[m];
@@ -773,7 +702,6 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
         }
 #undef SRCNN_D1_XB
       }
-      SRCNN_D1_TICK(5);
       __builtin_amdgcn_wave_barrier();
     }
   }
@@ -781,14 +709,6 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
 #undef SRCNN_D1_DMA_ALL
 #undef SRCNN_D1_X_DMA
 
-#ifdef SRCNN_D1_TIMING
-  if (lane == 0) {
-    const unsigned long long c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
-    for (int k = 0; k < 6; k++) g_d1_timing[blockIdx.x][wave][k] = tacc[k];
-    g_d1_timing[blockIdx.x][wave][6] = c1 - c0;
-    g_d1_timing[blockIdx.x][wave][7] = r1 - r0;
-  }
-#endif
   SRCNN_CLOCK_END(g_clk, 2);
   // ---- block reduction (waves in order) into LDS, then one slab per block ----
   __syncthreads();
@@ -860,9 +780,6 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
     }
   }
 }
-#ifndef SRCNN_D1C
-#define SRCNN_D1C 1  // n1 = 64, n2 = 32: kernel 3 in the cooperative-chunk form (d1c.hpp)
-#endif
 #include "d1c.hpp"
 
 // ---------------------------------------------------------------------------
@@ -872,15 +789,9 @@ __global__ __launch_bounds__(256, 2) void d1_grad12_kernel(
 // kernels in one launch: blocks [first[k], first[k+1]) serve segment k,
 // kSlabCols columns each, 64 row lanes per column (enough blocks to spread
 // over every CU).  SlabSeg / reduce_slabs are declared in ops.hpp.
-#ifndef SRCNN_SLAB_COLS
-#define SRCNN_SLAB_COLS 32  // wide net slab reduce 42 -> 33 us; fused neutral (same-box A/B)
-#endif
-constexpr int kSlabCols = SRCNN_SLAB_COLS;
+constexpr int kSlabCols = 32;  // wide net slab reduce 42 -> 33 us at 32 vs 16; fused neutral (same-box A/B)
 constexpr int kSlabRows = 1024 / kSlabCols;
-#ifndef SRCNN_SLAB_INFLIGHT
-#define SRCNN_SLAB_INFLIGHT 8
-#endif
-constexpr int kSlabInflight = SRCNN_SLAB_INFLIGHT;
+constexpr int kSlabInflight = 8;  // 16 / 32 loads in flight measured slower
 struct SlabSegs {
   SlabSeg seg[kMaxSlabSegs];
   int first[kMaxSlabSegs + 1];
@@ -975,19 +886,29 @@ struct Net {
 
 static int grid_for_batch(uint32_t batch, int cap) { return (int)std::min<uint32_t>(batch, cap); }
 
-template <int F3>
+template <int F3, int kUnits, bool kSplit>
 static int launch_l3r(const float* A2, const float* T, const float* W3, const float* B3, float* D2,
                       float* slab3, float* sqs, float* A3, const L3Geom& lg, int grid, size_t lds,
                       hipStream_t s) {
   // 70 KB exceeds the 64 KiB default dynamic LDS (set per launch: see launch_l3)
-  hipError_t e = hipFuncSetAttribute((const void*)l3r_delta_kernel<F3>,
+  hipError_t e = hipFuncSetAttribute((const void*)l3r_delta_kernel<F3, kUnits, kSplit>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
   if (e != hipSuccess)
     return fail(SRCNN_ERR_HIP, "hipFuncSetAttribute(l3r_delta): %s", hipGetErrorString(e));
-  hipLaunchKernelGGL((l3r_delta_kernel<F3>), dim3(grid), dim3(kL3RThreads), lds, s, A2, T, W3, B3,
-                     D2, slab3, sqs, A3, lg);
+  hipLaunchKernelGGL((l3r_delta_kernel<F3, kUnits, kSplit>), dim3(grid), dim3(kL3RThreads), lds, s, A2, T,
+                     W3, B3, D2, slab3, sqs, A3, lg);
   SRCNN_LAUNCH_TRY();
   return SRCNN_OK;
+}
+
+// below this batch, l3r runs half-sample items (l3r.hpp: l3r_split_row), so
+// that a small shard still fills two blocks per CU
+static int l3r_split_below() {
+  static const int v = [] {
+    const char* e = getenv("SRCNN_L3R_SPLIT_BELOW");
+    return e ? atoi(e) : 1024;
+  }();
+  return v;
 }
 
 template <int N2, int F3>
@@ -1023,20 +944,27 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   // keep l12 and d1 and run layer 3 through the op-level kernels instead
   // (ops_fast.hip: L3 forward, last delta, delta2, gW3 over HWC A2 / A3 / D3).
   // n2 = 32: l3r (A2 in registers, two blocks per CU) where the tile fits it
-  const bool l3r = SRCNN_L3R && N2 == 32 && l3r_fits<F3>(ow, oh, w3, h3);
-  const size_t lds3 = l3r ? L3RLds<F3>(ow, oh).bytes() : l3_lds_bytes<N2, F3>(ow, oh);
+  const bool l3r = N2 == 32 && l3r_fits<F3>(ow, oh, w3, h3);
+  const bool l3split = l3r && (int)batch < l3r_split_below() && l3r_split_fits<F3>(ow, oh, w3, h3);
+  const size_t lds3 = l3split ? L3RLds<F3, kL3RUnitsHalf, true>(ow, oh).bytes()
+                      : l3r   ? L3RLds<F3>(ow, oh).bytes()
+                              : l3_lds_bytes<N2, F3>(ow, oh);
+  // (n2 = 32: l3r takes every tile l3_delta's two LDS images would)
   const bool l3_fused =
-      l3r || (lds3 <= 160 * 1024 && w3 * h3 <= kL3MaxOut &&
+      l3r || (N2 != 32 && lds3 <= 160 * 1024 && w3 * h3 <= kL3MaxOut &&
               ((ow * oh + 15) / 16 + kL3Threads / 64 - 1) / (kL3Threads / 64) <= L3Lds<N2, F3>::kUnitsPerWave);
-  const int g12 = grid_for_batch(batch, SRCNN_L12_GRID);
+  const int g12 = grid_for_batch(batch, kL12Grid);
   // l3r: up to 2 resident blocks per CU; between 256 and 1024 samples keep
   // two samples per block, so the second sample's A2 loads run under the first
   // one's delta2 phase (512 tiles: l3 0.0306 -> 0.0295 ms; at batch 4096 a
   // 256-block grid is slower, 0.155 -> 0.167 ms; profiles/r04_ab_l3rgrid)
   const int b3 = (int)batch;
-  const int g3 = l3r ? std::min(SRCNN_L3R_GRID, std::max(std::min(b3, 256), (b3 + 1) / 2))
-                     : grid_for_batch(batch, 256);
-  const bool kD1c = SRCNN_D1C && N1 == 64 && N2 == 32 && F1 == 9 && d1c_fits(w, h);
+  // half-sample items: 2 * batch of them, an even grid (a block's items are
+  // all top or all bottom halves)
+  const int g3 = l3split ? std::min(kL3RGrid, 2 * b3)
+                 : l3r   ? std::min(kL3RGrid, std::max(std::min(b3, 256), (b3 + 1) / 2))
+                         : grid_for_batch(batch, 256);
+  const bool kD1c = N1 == 64 && N2 == 32 && F1 == 9 && d1c_fits(w, h);
   // d1c below kD1cGrid samples: each sample's chunks split into `parts`
   // ranges (work items), so the grid still fills every CU's 4 block slots
   const int nch1 = (ow * oh + 31) / 32;
@@ -1075,6 +1003,7 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   Geom g{(int)w, (int)h, ow, oh, (int)batch};
   {
     SRCNN_PROFILE("l12_fwd_mfma", s);
+    kernels_note(lazy ? "l12_fwd_lazy" : "l12_fwd");
     if (lazy)
       hipLaunchKernelGGL((l12_fwd_kernel<N1, N2, F1, true>), dim3(g12), dim3(256), 0, s, X, W1,
                          B1, W2, B2, A1, A2, g, *lz);
@@ -1090,11 +1019,17 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   L3Geom lg{(int)w, (int)h, ow, oh, w3, h3, (int)batch};
   if (l3_fused) {
     SRCNN_PROFILE("l3_delta_fused", s);
-    int rc = l3r ? launch_l3r<F3>(A2, T, W3, B3, D2, slab3, sqs, A3, lg, g3, lds3, s)
-                 : launch_l3<N2, F3>(A2, T, W3, B3, D2, slab3, sqs, A3, lg, g3, lds3, s);
+    kernels_note(l3split ? "l3r_delta_split" : l3r ? "l3r_delta" : "l3_delta");
+    int rc;
+    if constexpr (N2 == 32)
+      rc = l3split ? launch_l3r<F3, kL3RUnitsHalf, true>(A2, T, W3, B3, D2, slab3, sqs, A3, lg, g3, lds3, s)
+                   : launch_l3r<F3, kL3RUnits, false>(A2, T, W3, B3, D2, slab3, sqs, A3, lg, g3, lds3, s);
+    else
+      rc = launch_l3<N2, F3>(A2, T, W3, B3, D2, slab3, sqs, A3, lg, g3, lds3, s);
     if (rc) return rc;
   } else {
     // ConfigBasedDataPipeline.cpp:200-323 for layer 3 on the op-level kernels
+    kernels_note("l3_op_level");
     const int rf = fast::try_conv_fwd(A2, A3, W3, B3, ow, oh, N2, 1, F3, 0, batch, s);
     if (rf != 1) return rf < 0 ? rf : fail(SRCNN_ERR_INVALID, "fused step: no layer-3 kernel for %dx%d", ow, oh);
     if (sq_err)
@@ -1110,6 +1045,7 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   }
   {
     SRCNN_PROFILE("delta1_grad12_fused", s);
+    kernels_note(kD1c ? "d1c_grad12" : "d1_grad12");
     if (kD1c)
       hipLaunchKernelGGL((d1c_grad12_kernel<(F1 == 9 ? F1 : 9)>), dim3(gd), dim3(256 * kD1cTeams), d1c_lds_bytes(w, h),
                          s, X, A1, D2, W2, slab12, g, d1c_xs_floats(h), d1c_parts);
@@ -1120,6 +1056,7 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   }
   {
     SRCNN_PROFILE("slab_reduce", s);
+    kernels_note(up && l3_fused ? "slab_reduce_update" : "slab_reduce");
     const SlabSeg segs[3] = {{slab12, grads, gd, NetT::P12, 0},
                              {slab3, grads + NetT::P12, g3, NetT::P3, 0},
                              {sqs, sq_err, g3, 1, 0}};
@@ -1156,11 +1093,19 @@ static int preload_one(const srcnn_net* net) {
   if (net->n1 != (uint32_t)N1 || net->n2 != (uint32_t)N2 || net->f1 != (uint32_t)F1 ||
       net->f2 != 1 || net->f3 != (uint32_t)F3)
     return 0;
-  const void* k[] = {(const void*)l12_fwd_kernel<N1, N2, F1>, (const void*)l12_fwd_kernel<N1, N2, F1, true>,
-                     (const void*)l3_delta_kernel<N2, F3>, (const void*)d1_grad12_kernel<N1, N2, F1>,
-                     (const void*)slab_reduce_kernel, (const void*)l3r_delta_kernel<F3>,
-                     (const void*)d1c_grad12_kernel<9>};
-  int rc = resolve_kernels(k, SRCNN_D1C && N1 == 64 && N2 == 32 && F1 == 9 ? 7 : 6);
+  int rc;
+  if constexpr (N2 == 32) {
+    const void* k[] = {(const void*)l12_fwd_kernel<N1, N2, F1>, (const void*)l12_fwd_kernel<N1, N2, F1, true>,
+                       (const void*)d1_grad12_kernel<N1, N2, F1>, (const void*)slab_reduce_kernel,
+                       (const void*)l3r_delta_kernel<F3>, (const void*)l3r_delta_kernel<F3, kL3RUnitsHalf, true>,
+                       (const void*)d1c_grad12_kernel<9>};
+    rc = resolve_kernels(k, N1 == 64 && F1 == 9 ? 7 : 6);
+  } else {
+    const void* k[] = {(const void*)l12_fwd_kernel<N1, N2, F1>, (const void*)l12_fwd_kernel<N1, N2, F1, true>,
+                       (const void*)l3_delta_kernel<N2, F3>, (const void*)d1_grad12_kernel<N1, N2, F1>,
+                       (const void*)slab_reduce_kernel};
+    rc = resolve_kernels(k, 5);
+  }
   return rc ? rc : 1;
 }
 
@@ -1228,19 +1173,3 @@ int train_fwd_bwd(const srcnn_net* net, const float* X, const float* T, uint32_t
 }  // namespace fused
 }  // namespace srcnn
 
-#ifdef SRCNN_D1_TIMING
-extern "C" __attribute__((visibility("default"))) int srcnn_debug_d1_timing(unsigned long long* out) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(srcnn::fused::g_d1_timing), sizeof(srcnn::fused::g_d1_timing)) ==
-                 hipSuccess
-             ? 0
-             : -1;
-}
-#endif
-#ifdef SRCNN_L3_TIMING
-extern "C" __attribute__((visibility("default"))) int srcnn_debug_l3_timing(unsigned long long* out) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(srcnn::fused::g_l3_timing), sizeof(srcnn::fused::g_l3_timing)) ==
-                 hipSuccess
-             ? 0
-             : -1;
-}
-#endif

@@ -105,6 +105,7 @@ SIGNATURES = {
     "srcnn_set_path": (_I, [_I]),
     "srcnn_get_path": (_I, []),
     "srcnn_last_path": (ctypes.c_char_p, []),
+    "srcnn_last_kernels": (ctypes.c_char_p, []),
     "srcnn_comm_id": (_I, [ctypes.c_char_p]),
     "srcnn_comm_init_rank": (_I, [ctypes.POINTER(_P), _I, ctypes.c_char_p, _I]),
     "srcnn_comm_init_all": (_I, [ctypes.POINTER(_P), _I, ctypes.POINTER(_I)]),
@@ -407,6 +408,13 @@ def preload(net):
     """Resolve the net's gfx950 kernels on the current device (srcnn_preload):
     the runtime's lazy kernel setup happens here, not in the first step."""
     _call("srcnn_preload", ctypes.byref(net))
+
+
+def last_kernels():
+    """Kernel variants of this thread's most recent training call, as a list
+    (srcnn_last_kernels), e.g. ["l12_fwd", "l3r_delta", "d1c_grad12", ...]."""
+    v = _lib.srcnn_last_kernels().decode()
+    return v.split(",") if v else []
 
 
 def last_path():

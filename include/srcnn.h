@@ -261,6 +261,11 @@ SRCNN_API int srcnn_get_path(void);
  *   "generic" ops_generic.hip (any shape; one thread per output)
  *   ""        nothing launched yet on this thread */
 SRCNN_API const char* srcnn_last_path(void);
+/* The kernels, by variant, that this thread's most recent training call
+ * (srcnn_train_fwd_bwd / _step / _lazy) launched, comma-separated, e.g.
+ * "l12_fwd,l3r_delta_split,d1c_grad12,slab_reduce" -- so that a test can
+ * assert which specialisation served a shape.  "" before any such call. */
+SRCNN_API const char* srcnn_last_kernels(void);
 
 /* One training step on one device: srcnn_train_fwd_bwd over the batch, then
  * srcnn_update_all(update_batch) -- src/Main_cl.cpp:161-175 (execute_batch

@@ -520,14 +520,22 @@ def test_train_step_nonsquare_tiles(S, w, h, batch):
         assert_close(got[sl], rg[sl], RTOL, "grad " + nm, xg[sl], FLIP_FLOOR)
 
 
-@pytest.mark.parametrize("batch,w,h", [(16, 33, 33), (512, 33, 33), (257, 33, 33), (7, 35, 31), (3, 39, 39),
-                                       (2, 21, 21)])
-def test_train_step_sq_err_and_a3_vs_oracle(S, batch, w, h):
-    """The fused step's layer 3 (l3_delta_kernel): gradients, squared error
-    and the A3 it leaves in the workspace (srcnn_train_activations) against
-    the oracle (last_layer_delta.cl, squared_error.cl, layer_deltas.cl,
-    backpropagate.cl)."""
-    cfg = NETS["default"]
+@pytest.mark.parametrize("name,batch,w,h,l3", [
+    # below 1024 samples l3r runs half-sample items (top / bottom A3 rows, the
+    # bottom item recomputing the 4-row delta3 halo its delta2 rows need)
+    ("default", 16, 33, 33, "l3r_delta_split"), ("default", 512, 33, 33, "l3r_delta_split"),
+    ("default", 257, 33, 33, "l3r_delta_split"), ("default", 7, 35, 31, "l3r_delta_split"),
+    ("default", 2, 21, 21, "l3r_delta_split"),
+    # whole-sample l3r items
+    ("default", 1024, 33, 33, "l3r_delta"), ("default", 1537, 33, 33, "l3r_delta"),
+    # n2 = 16: l3_delta; past 640 A2 pixels: the op-level layer-3 kernels
+    ("example", 16, 33, 33, "l3_delta"), ("default", 3, 39, 39, "l3_op_level")])
+def test_train_step_sq_err_and_a3_vs_oracle(S, name, batch, w, h, l3):
+    """The fused step's layer-3 kernel -- which one ran is asserted per case
+    (srcnn_last_kernels): gradients, squared error and the A3 it leaves in the
+    workspace (srcnn_train_activations) against the oracle
+    (last_layer_delta.cl, squared_error.cl, layer_deltas.cl, backpropagate.cl)."""
+    cfg = NETS[name]
     net = S.Net(*cfg)
     rng = np.random.default_rng(31)
     X, T = make_batch(rng, batch, w, h)
@@ -541,6 +549,7 @@ def test_train_step_sq_err_and_a3_vs_oracle(S, batch, w, h):
     g, err = D(g0), zeros(1)
     S.train_fwd_bwd(net, D(X), D(T), w, h, batch, D(params), g, err, ws, nbytes)
     assert S.last_path() == "fused", S.last_path()
+    assert l3 in S.last_kernels(), S.last_kernels()
     got = H(g)
     off = S.net_offsets(net) + [P]
     for i, nm in enumerate(["W1", "B1", "W2", "B2", "W3", "B3"]):

@@ -1,0 +1,125 @@
+"""Issue-slot accounting of a kernel's innermost hot loop from its gfx950 ISA.
+
+    python tools/isa_budget.py <file.s> <kernel-name-substring> [--mfma-cycles 32]
+
+Builds the assembly of a source with
+    hipcc --offload-arch=gfx950 -O3 ... --cuda-device-only -S -o file.s
+finds the kernel, splits it into basic blocks, finds loops by their
+back-edges (an s_cbranch / s_branch to an earlier label of the kernel), and
+for every loop that holds MFMAs prints the instruction classes of its body:
+MFMA (with their matrix-pipe cycles), VALU, SALU, LDS reads / writes, vector
+memory (loads, stores, LDS-DMA), s_waitcnt, barriers, branches.  Nested loops
+count into the outer loop once per static instruction (a static count, not a
+trace)."""
+import re
+import sys
+from collections import Counter, OrderedDict
+
+# matrix-pipe cycles per MFMA (MI355X_MICROARCH.md: 16x16x4 f32 issues every
+# 32 cycles when independent; 32x32x2 f32 every 64)
+MFMA_CYCLES = {"v_mfma_f32_16x16x4_f32": 32, "v_mfma_f32_16x16x4f32": 32,
+               "v_mfma_f32_32x32x2_f32": 64, "v_mfma_f32_32x32x2f32": 64}
+
+
+def classify(op):
+    if op.startswith("v_mfma"):
+        return "mfma"
+    if op.startswith("ds_read") or op.startswith("ds_load"):
+        return "lds_read"
+    if op.startswith("ds_write") or op.startswith("ds_store"):
+        return "lds_write"
+    if op.startswith("ds_"):
+        return "lds_other"
+    if op.startswith("global_load_lds") or op.startswith("buffer_load") and "lds" in op:
+        return "vmem_dma"
+    if op.startswith("global_load") or op.startswith("buffer_load") or op.startswith("flat_load") \
+            or op.startswith("scratch_load"):
+        return "vmem_load"
+    if op.startswith("global_store") or op.startswith("buffer_store") or op.startswith("flat_store") \
+            or op.startswith("scratch_store"):
+        return "vmem_store"
+    if op.startswith("s_waitcnt"):
+        return "waitcnt"
+    if op.startswith("s_barrier"):
+        return "barrier"
+    if op.startswith("s_cbranch") or op.startswith("s_branch"):
+        return "branch"
+    if op.startswith("s_nop") or op.startswith("s_sched") or op.startswith("s_setprio"):
+        return "nop"
+    if op.startswith("s_"):
+        return "salu"
+    if op.startswith("v_"):
+        return "valu"
+    return "other"
+
+
+def kernel_lines(path, name):
+    lines = open(path).read().split("\n")
+    start = None
+    for i, ln in enumerate(lines):
+        if ln.startswith("_Z") and ln.split(":")[0].find(name) >= 0 and ln.rstrip().endswith(
+                ln.split(":")[0] + ":") is False:
+            pass
+        if re.match(r"^_Z\S*%s\S*:" % re.escape(name), ln):
+            start = i
+            break
+    if start is None:
+        raise SystemExit("kernel %s not found" % name)
+    out = []
+    for ln in lines[start + 1:]:
+        if ln.startswith("\t.section") or re.match(r"^\.Lfunc_end", ln):
+            break
+        out.append(ln)
+    return out
+
+
+def main():
+    path, name = sys.argv[1], sys.argv[2]
+    lines = kernel_lines(path, name)
+    blocks = OrderedDict()
+    cur = "entry"
+    blocks[cur] = []
+    order = [cur]
+    for ln in lines:
+        m = re.match(r"^(\.LBB\w+):", ln)
+        if m:
+            cur = m.group(1)
+            blocks[cur] = []
+            order.append(cur)
+            continue
+        s = ln.strip()
+        if not s or s.startswith(";") or s.startswith("."):
+            continue
+        op = s.split()[0]
+        blocks[cur].append((op, s))
+    pos = {b: i for i, b in enumerate(order)}
+    loops = []
+    for i, b in enumerate(order):
+        for op, s in blocks[b]:
+            if op.startswith("s_cbranch") or op.startswith("s_branch"):
+                tgt = s.split()[-1]
+                if tgt in pos and pos[tgt] <= i:
+                    loops.append((pos[tgt], i))
+    seen = set()
+    for a, z in sorted(loops, key=lambda t: t[1] - t[0]):
+        if (a, z) in seen:
+            continue
+        seen.add((a, z))
+        c = Counter()
+        mcyc = 0
+        for b in order[a:z + 1]:
+            for op, s in blocks[b]:
+                k = classify(op)
+                c[k] += 1
+                if k == "mfma":
+                    mcyc += MFMA_CYCLES.get(op, 32)
+        if c["mfma"] == 0:
+            continue
+        non_mfma = sum(v for k, v in c.items() if k not in ("mfma", "nop"))
+        print("loop %s..%s (%d blocks): %s" % (order[a], order[z], z - a + 1, dict(sorted(c.items()))))
+        print("   MFMA %d = %d matrix-pipe cycles; other issued instructions %d "
+              "(%.2f per MFMA)" % (c["mfma"], mcyc, non_mfma, non_mfma / c["mfma"]))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,4 +1,5 @@
-# wgrad2 band-halo A/B: wide parity + bench per variant, then the HBM-byte
+# Wide-net A/B of library builds (tools/build_variant.sh, one per source tree
+# or flag set): wide parity + bench per variant, then the HBM-byte
 # passes (FETCH_SIZE, WRITE_SIZE) per variant.  Variants as arguments.
 cd $GRAFT_REPO_ROOT
 V=${@:-"nohalo halo"}
