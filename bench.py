@@ -329,7 +329,7 @@ def cpu_forward_baseline(net, strip_rows=256, reps=3):
     return out
 
 
-def forward_4k(S, net_t, frames=20, warmup=3, w=3840, h=2160):
+def forward_4k(S, net_t, frames=20, warmup=3, w=3840, h=2160, settle_ms=50.0):
     """BASELINE.json configs[4]: forward-only inference of one 3840x2160 luma
     frame (fused path), reported as input Mpix/s.  Time with events on the
     stream the kernels run on; per-kernel split from srcnn_profile_*."""
@@ -343,6 +343,11 @@ def forward_4k(S, net_t, frames=20, warmup=3, w=3840, h=2160):
     out = torch.empty((w - (f1 + f2 + f3 - 3)) * (h - (f1 + f2 + f3 - 3)), device=dev)
     nbytes = S.forward_workspace_bytes(net, w, h, 1)
     ws = torch.empty(nbytes // 4 + 64, device=dev)
+    # the frames follow the 0.5 s pause after the wide net: without settle()
+    # they time the clock ramp (rocprofv3, profiles/r05_clock: 1.19 -> 1.03 ms
+    # for the first 20 frames' fwd_l123)
+    n_settle = settle(lambda: S.forward(net, x, w, h, 1, prm, out, ws, nbytes, stream), settle_ms,
+                      torch.cuda.synchronize, 1, "gloo", dev)
     for _ in range(warmup):
         S.forward(net, x, w, h, 1, prm, out, ws, nbytes, stream)
     torch.cuda.synchronize()
@@ -371,7 +376,7 @@ def forward_4k(S, net_t, frames=20, warmup=3, w=3840, h=2160):
         kroof = {"bound": "mfma", "achieved": round(ach, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                  "frac": round(ach / PEAK_FP32_TFLOPS, 4), "kernel": kname, "avg_launch_ms": round(kdur * 1e3, 5),
                  "algorithmic_flops_per_launch": int(flops), "traffic": None}
-    res = {"frame": "%dx%d" % (w, h), "frames": frames, "ms_per_frame": round(ms, 4),
+    res = {"frame": "%dx%d" % (w, h), "frames": frames, "settle_frames": n_settle, "ms_per_frame": round(ms, 4),
            "mpix_s": round(w * h / (ms * 1e-3) / 1e6, 1),
            "tflops": round(flops / (ms * 1e-3) / 1e12, 2),
            "roofline_frac": round(flops / (ms * 1e-3) / 1e12 / PEAK_FP32_TFLOPS, 4),
@@ -411,7 +416,8 @@ def forward_tile_256(S, net_t, reps=20):
             "kernel_path": S.last_path(), "reps": reps}
 
 
-def forward_4k_sharded(S, net_t, rank, world, reduce_max, frames=10, warmup=3, w=3840, h=2160):
+def forward_4k_sharded(S, net_t, rank, world, reduce_max, backend, frames=10, warmup=3, w=3840, h=2160,
+                       settle_ms=50.0):
     """BASELINE.json configs[4] on N GPUs: the 3840x2160 frame sharded by row
     bands with a 12-row halo (parallel.forward_band), no
     collective in the data path.  Every rank holds the frame and writes its
@@ -428,6 +434,8 @@ def forward_4k_sharded(S, net_t, rank, world, reduce_max, frames=10, warmup=3, w
     _, ni, _, _ = parallel.frame_band(w, h, net_t[2:], rank, world)
     nbytes = S.forward_workspace_bytes(net, w, max(ni, ctx + 1), 1)
     ws = torch.empty(nbytes // 4 + 64, device=dev)
+    settle(lambda: parallel.forward_band(S, net, x, w, h, prm, out, ws, nbytes, stream, rank, world),
+           settle_ms, torch.cuda.synchronize, world, backend, dev)
     for _ in range(warmup):
         parallel.forward_band(S, net, x, w, h, prm, out, ws, nbytes, stream, rank, world)
     torch.cuda.synchronize()
@@ -942,7 +950,7 @@ def run(args, S, parallel, rank, world, local, device=None):
             t = torch.tensor([v], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             return float(t.item())
-        fwd_sharded = forward_4k_sharded(S, net_t, rank, world, reduce_max)
+        fwd_sharded = forward_4k_sharded(S, net_t, rank, world, reduce_max, backend)
 
     if rank == 0:
         K = args.steps

@@ -90,15 +90,7 @@ namespace srcnn {
 // still believed older loads outstanding and, at their first use, emitted a
 // vmcnt(N) that waited for the DMA just issued.  After this one it knows them
 // complete and emits no such wait.
-#ifndef SRCNN_VISIBLE_WAIT
-#define SRCNN_VISIBLE_WAIT 1
-#endif
-__device__ __forceinline__ void wait_vm0() {
-  if (SRCNN_VISIBLE_WAIT)
-    __builtin_amdgcn_s_waitcnt(0x0F70);
-  else
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
+__device__ __forceinline__ void wait_vm0() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 constexpr int kClockBlocks = 8;
 #ifdef SRCNN_CLOCK_PROBE
 constexpr bool kClockProbe = true;

@@ -38,29 +38,13 @@ __device__ unsigned long long g_clk_fwd[1][kClockBlocks][2];
 namespace {
 
 constexpr int kFwdRW = 32;        // region width (one chunk per region row)
-#ifndef SRCNN_FWD_RH
-#define SRCNN_FWD_RH 28
-#endif
-#ifndef SRCNN_FWD_WAVES
-#define SRCNN_FWD_WAVES 2  // minimum waves per SIMD (register budget 512 / this)
-#endif
-#ifndef SRCNN_FWD_GRID
-#define SRCNN_FWD_GRID 2048
-#endif
-#ifndef SRCNN_FWD_PD
-#define SRCNN_FWD_PD 4  // L1 X-gather prefetch distance (k-steps); 0 = compiler schedule
-#endif
-constexpr int kFwdPD = SRCNN_FWD_PD;
+constexpr int kFwdPD = 4;      // L1 X-gather prefetch distance (k-steps), pinned by sched barriers
+constexpr int kFwdGrid = 2048;  // grid cap (blocks)
 
 // diagnostics builds only (results invalid): 1 drop the per-chunk L3 window
 // sums, 2 drop the per-region partial-sum output, 4 drop the ReLUs, 8 drop the
 // next region's register-staged input loads
-#ifdef SRCNN_FWD_DIAG
-constexpr int kFwdDiag = SRCNN_FWD_DIAG;
-#else
-constexpr int kFwdDiag = 0;
-#endif
-constexpr int kFwdRhMax = SRCNN_FWD_RH;  // region rows (LDS partial-sum accumulator bound)
+constexpr int kFwdRhMax = 28;  // region rows (LDS partial-sum accumulator bound)
 constexpr int kFwdXs = (kFwdRhMax + 12) * 40;  // input tile floats staged in LDS (f1 <= 9)
 
 struct FwdGeom {
@@ -72,7 +56,7 @@ struct FwdGeom {
 };
 
 template <int N1, int N2, int F1, int F3>
-__global__ __launch_bounds__(256, SRCNN_FWD_WAVES) void fwd_l123_kernel(
+__global__ __launch_bounds__(256, 2) void fwd_l123_kernel(
     const float* __restrict__ X, const float* __restrict__ W1, const float* __restrict__ B1,
     const float* __restrict__ W2, const float* __restrict__ B2, const float* __restrict__ W3,
     float* __restrict__ part, FwdGeom g) {
@@ -171,7 +155,6 @@ __global__ __launch_bounds__(256, SRCNN_FWD_WAVES) void fwd_l123_kernel(
     }
   };
   if ((int)blockIdx.x < n_items) xload(blockIdx.x);
-  float diag_sink = 0.0f;  // diagnostics builds: keeps dropped parts' inputs live
   for (int wi = blockIdx.x; wi < n_items; wi += gridDim.x) {
     const int n = wi / per_frame, rr = wi - n * per_frame;
     const int ry = rr / g.nrx;
@@ -185,8 +168,30 @@ __global__ __launch_bounds__(256, SRCNN_FWD_WAVES) void fwd_l123_kernel(
       if (i < kFwdXs) xs[i] = xr[k];
     }
     __syncthreads();
-    if (wi + (int)gridDim.x < n_items && !(kFwdDiag & 8)) xload(wi + gridDim.x);
+    if (wi + (int)gridDim.x < n_items) xload(wi + gridDim.x);
 
+    // The L3 window sums of a chunk run inside this wave's NEXT chunk's L1
+    // MFMA stream (its Q^T stays in the wave's scratch until that chunk's own
+    // Q overwrites it): read at k-steps kWinS + kWinD k, summed and stored
+    // kWinD / 2 steps later.  Issued after the Q MFMAs they were a ~500-cycle
+    // LDS / VALU tail per chunk with no MFMA of this wave behind it.
+    constexpr int kWinS = 2, kWinD = (KS1 - kWinS - 4) / kWin;
+    static_assert(kWinD >= 2 && kWinS + kWinD * kWin + kWinD / 2 < KS1, "window sums fit the L1 stream");
+    auto win_read = [&](int k, float* v) {
+      const float* qr = &qs[0][0][0] + wrb[k];
+#pragma unroll
+      for (int dx = 0; dx < F3; dx++) v[dx] = qr[dx * (QTS + 1)];
+    };
+    auto win_store = [&](int k, const float* v, int pc) {
+      if (k < kWin - 1 || lane + 64 * k < F3 * EW) {
+        float t = 0.0f;
+#pragma unroll
+        for (int dx = 0; dx < F3; dx++) t += v[dx];
+        (&accs[0][0][0])[wwb[k] + pc * EW] = t;
+      }
+    };
+    int pc = -1;  // this wave's chunk whose window sums are pending (wave-uniform)
+    float wv_last[F3];
     for (int c = wave; c < crh; c += 4) {  // chunk = region row c, pixel li
       // tap 2s+1 sits 1 or TW - F1 + 1 floats past tap 2s: two per-half bases,
       // every gather is base + immediate
@@ -205,22 +210,29 @@ __global__ __launch_bounds__(256, SRCNN_FWD_WAVES) void fwd_l123_kernel(
       // barriers: left alone, the scheduler issues each one just before its
       // MFMA pair and the wave waits out the full LDS latency every step
       float xq[KS1];
+      float wv[F3];
 #pragma unroll
       for (int s = 0; s < kFwdPD && s < KS1; s++) xq[s] = xg(s);
 #pragma unroll
       for (int s = 0; s < KS1; s++) {
         if (s + kFwdPD < KS1) xq[s + kFwdPD] = xg(s + kFwdPD);
-        if (kFwdPD > 0) __builtin_amdgcn_sched_barrier(0);
-        const float xv = kFwdPD > 0 ? xq[s] : xg(s);
+        if (pc >= 0 && s >= kWinS && (s - kWinS) % kWinD == 0 && (s - kWinS) / kWinD < kWin)
+          win_read((s - kWinS) / kWinD, wv);
+        __builtin_amdgcn_sched_barrier(0);
+        const float xv = xq[s];
 #pragma unroll
         for (int t = 0; t < NT1; t++) acc1[t] = mma(w1f[s][t], xv, acc1[t]);
+        if (pc >= 0 && s >= kWinS + kWinD / 2 && (s - kWinS - kWinD / 2) % kWinD == 0 &&
+            (s - kWinS - kWinD / 2) / kWinD < kWin)
+          win_store((s - kWinS - kWinD / 2) / kWinD, wv, pc);
+        __builtin_amdgcn_sched_barrier(0);
       }
       // L1 ReLU (layer_uber_kernel.cl:88-95; bias already in)
 #pragma unroll
       for (int t = 0; t < NT1; t++)
 #pragma unroll
         for (int r = 0; r < 16; r++)
-          if (!(kFwdDiag & 4)) acc1[t][r] = fmaxf(acc1[t][r], 0.0f);
+          acc1[t][r] = fmaxf(acc1[t][r], 0.0f);
       // L2^T: A2^T[n][p] = B2[n] + sum_c W2[c][n] A1^T[c][p], then ReLU
       f32x16 acc2;
 #pragma unroll
@@ -235,36 +247,31 @@ __global__ __launch_bounds__(256, SRCNN_FWD_WAVES) void fwd_l123_kernel(
         for (int s = 0; s < 16; s++) acc2 = mma(w2f[t][s], acc1[t][s], acc2);
 #pragma unroll
       for (int r = 0; r < 16; r++)
-        if (!(kFwdDiag & 4)) acc2[r] = fmaxf(acc2[r], 0.0f);
+        acc2[r] = fmaxf(acc2[r], 0.0f);
       // Q^T[tap][p] = sum_c W3[tap][c] A2^T[c][p]
       f32x16 accq = zero16();
 #pragma unroll
       for (int s = 0; s < 16; s++) accq = mma(w3f[s], acc2[s], accq);
       // Q^T[taps crow(r, h)][pixel li]: 16 rows per lane, lanes consecutive
+      // (the pending window sums above read the previous Q^T: their values
+      // are summed, so those reads have completed)
 #pragma unroll
       for (int r = 0; r < 16; r++) qs[wave][crow(r, h)][li + F3 - 1] = accq[r];
       __builtin_amdgcn_wave_barrier();
-      // tap row dy of this chunk feeds partial row c + F3 - 1 - dy:
-      //   accs[dy][c + F3-1 - dy][e] = sum_dx Q[e - (F3-1) + dx][dy*F3 + dx]
-      if (kFwdDiag & 1) {  // keep Q alive without its window sums
-#pragma unroll
-        for (int r = 0; r < 16; r++) diag_sink += accq[r];
-      }
-      //   (Q row e + dx of the padded image is pixel e - (F3-1) + dx)
+      pc = c;
+    }
+    // tap row dy of a chunk feeds partial row c + F3 - 1 - dy:
+    //   accs[dy][c + F3-1 - dy][e] = sum_dx Q[e - (F3-1) + dx][dy*F3 + dx]
+    //   (Q row e + dx of the padded image is pixel e - (F3-1) + dx)
+    // here the window sums of this wave's last chunk
+    if (pc >= 0) {
 #pragma unroll
       for (int k = 0; k < kWin; k++) {
-        if (kFwdDiag & 1) break;
-        if (k < kWin - 1 || lane + 64 * k < F3 * EW) {
-          const float* qr = &qs[0][0][0] + wrb[k];
-          float v = 0.0f;
-#pragma unroll
-          for (int dx = 0; dx < F3; dx++) v += qr[dx * (QTS + 1)];
-          (&accs[0][0][0])[wwb[k] + c * EW] = v;
-        }
+        win_read(k, wv_last);
+        win_store(k, wv_last, pc);
       }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_wave_barrier();
     }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __syncthreads();
     // partial row pr gets tap rows dy whose chunk c = pr - (F3-1) + dy exists
     float* dst = part + (size_t)wi * EH * EW;
@@ -276,11 +283,9 @@ __global__ __launch_bounds__(256, SRCNN_FWD_WAVES) void fwd_l123_kernel(
         const int c = pr - (F3 - 1) + dy;
         if (c >= 0 && c < crh) v += accs[dy][pr][e];
       }
-      if (!(kFwdDiag & 2)) dst[i] = v;
-      else diag_sink += v;
+      dst[i] = v;
     }
   }
-  if (kFwdDiag && diag_sink == 1234.5f) part[threadIdx.x] = diag_sink;
   SRCNN_CLOCK_END(g_clk_fwd, 0);
 }
 
@@ -348,7 +353,7 @@ int run_forward(const float* X, uint32_t w, uint32_t h, uint32_t batch, const fl
   const float* B3 = W3 + F3 * F3 * N2;
   {
     SRCNN_PROFILE("fwd_l123_mfma", s);
-    hipLaunchKernelGGL((fwd_l123_kernel<N1, N2, F1, F3>), dim3((unsigned)std::min<long>(items, SRCNN_FWD_GRID)),
+    hipLaunchKernelGGL((fwd_l123_kernel<N1, N2, F1, F3>), dim3((unsigned)std::min<long>(items, kFwdGrid)),
                        dim3(256), 0, s, X, W1, B1, W2, B2, W3, part, g);
     SRCNN_LAUNCH_TRY();
   }

@@ -68,22 +68,9 @@ __device__ __forceinline__ void dma16(const float* src, float* lds_dst) {
                : "s"(__builtin_amdgcn_readfirstlane(lds_addr(lds_dst))), "v"(src)
                : "m0");
 }
-// the same DMA with the nontemporal hint, for input images each block reads
-// once (conv_mfma, d1g16), so they pass through L2 without evicting the
-// W2 operand images every block re-reads
-#ifndef SRCNN_WIDE_DMA_NT
-#define SRCNN_WIDE_DMA_NT 0
-#endif
-__device__ __forceinline__ void dma16_stream(const float* src, float* lds_dst) {
-#if SRCNN_WIDE_DMA_NT
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt"
-               :
-               : "s"(__builtin_amdgcn_readfirstlane(lds_addr(lds_dst))), "v"(src)
-               : "m0");
-#else
-  dma16(src, lds_dst);
-#endif
-}
+// (conv_mfma / d1g16 stage their input images with the default cache policy:
+// with the nontemporal hint the L2 forward's HBM bytes went 2.21 -> 3.09 GB
+// per launch and delta1's 2.23 -> 2.78 GB, profiles/r04_ab_widedmant)
 __device__ __forceinline__ void dma4(const float* src, float* lds_dst) {
   asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dword %1, off"
                :
@@ -320,7 +307,7 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restri
                     ((unsigned)x < (unsigned)g.in_w);
     const float* base = in + ((size_t)wn.s * g.in_h * g.in_w) * CIN + c * kCC;
     const float* src = ok ? base + (y * g.in_w + x) * CIN + 4 * q : g_zero_src;
-    dma16_stream(src, buf + k * 256);
+    dma16(src, buf + k * 256);
   };
   auto kdma_of = [](const CWin& wn) { return (wn.iw * wn.ih * 5 + 63) / 64; };
   float* const buf0 = smem;
@@ -478,12 +465,6 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restri
 //   channel n, i.e. directly gW1's B operand (K = the 4 pixel slots); A = the
 //   X windows of 16-tap tiles (81 taps + the ones row: 6 tiles)
 // ---------------------------------------------------------------------------
-#ifndef SRCNN_D16_XCD
-#define SRCNN_D16_XCD 1  // d1g16: a sample's two channel halves on one XCD
-#endif
-#ifndef SRCNN_D16_MASK_AHEAD
-#define SRCNN_D16_MASK_AHEAD 3  // epilogue relu' loads run this many tiles ahead
-#endif
 constexpr int kD16MT = 20;                   // 16-pixel tiles per wave group
 constexpr int kD16Slots = 2 * kD16MT * 16;  // pixel slots of the tile table
 template <int CIN, int COUT, int F, int F1>
@@ -504,12 +485,10 @@ __global__ __launch_bounds__(256, 1) void d1g16_kernel(const float* __restrict__
   // the NP parts of a sample (the same delta2 image) on one XCD: blocks go
   // round-robin over the 8 XCDs, so parts of pair k run as blocks x, x + 8
   int vb = blockIdx.x;
-#if SRCNN_D16_XCD
   if (gridDim.x % (8 * NP) == 0) {
     const int j = blockIdx.x / 8;
     vb = (blockIdx.x % 8 + 8 * (j / NP)) * NP + j % NP;
   }
-#endif
   float* const xsm = smem + 2 * buf_floats;  // 2 X tile buffers (item parity)
   int* const ptab = reinterpret_cast<int*>(xsm + 2 * kXBuf);
   // gW1 A operand: tap 16 tt + i16; tap NT1 - 1 (offset toffl) and gB1 by VALU
@@ -607,7 +586,7 @@ __global__ __launch_bounds__(256, 1) void d1g16_kernel(const float* __restrict__
                     ((unsigned)x < (unsigned)g.in_w);
     const float* base = in + ((size_t)s * g.in_h * g.in_w) * CIN + c * kCC;
     const float* src = ok ? base + (y * g.in_w + x) * CIN + 4 * q : g_zero_src;
-    dma16_stream(src, buf + k * 256);
+    dma16(src, buf + k * 256);
   };
   const int kdma = (g.img_w * g.img_h * 5 + 63) / 64;
   float* const buf0 = smem;
@@ -696,7 +675,7 @@ __global__ __launch_bounds__(256, 1) void d1g16_kernel(const float* __restrict__
     const size_t obase = (size_t)s * g.npx * COUT + part * 64 + nt * 32 + i16;
     // relu' operands (A1, from HBM) kEpD tiles ahead in a ring of named sets:
     // a tile's gW1 work (48 MFMAs) is shorter than one HBM round trip
-    constexpr int kEpD = SRCNN_D16_MASK_AHEAD;
+    constexpr int kEpD = 3;  // epilogue relu' loads this many tiles ahead
     float mk[kEpD + 1][2][4];
     auto ldmask = [&](int m, float (&d)[2][4]) {
 #pragma unroll
@@ -807,10 +786,7 @@ __global__ __launch_bounds__(256, 1) void d1g16_kernel(const float* __restrict__
 // current tile's MFMAs, and gW3's A2 pixel pairs come in batches of kWl3B, the
 // next batch in flight under the current one.  Two blocks per CU, every
 // accumulator in VGPRs (launch bound).
-#ifndef SRCNN_WL3_B
-#define SRCNN_WL3_B 4  // gW3 pixel pairs per prefetch batch
-#endif
-constexpr int kWl3B = SRCNN_WL3_B;
+constexpr int kWl3B = 4;  // gW3 pixel pairs per prefetch batch
 template <int N2, int F3>
 __global__ __launch_bounds__(256, 2) void wl3_kernel(const float* __restrict__ A2,
                                                   const float* __restrict__ T,
@@ -1194,12 +1170,6 @@ __global__ __launch_bounds__(512, 1) void wl3l_kernel(const float* __restrict__ 
 // delta2 rows (64 channels, 80-float pixels) are DMA'd into LDS, double
 // buffered across bands; the compute loop only reads LDS.
 // ---------------------------------------------------------------------------
-#ifndef SRCNN_WG2_XCD
-#define SRCNN_WG2_XCD 1  // a sample group's channel-quarter blocks on one XCD
-#endif
-#ifndef SRCNN_WG2_HALO
-#define SRCNN_WG2_HALO 1  // band halo rows copied LDS -> LDS from the previous band
-#endif
 constexpr int kGAS = 48;      // LDS floats per A1 pixel (32 channels + pad)
 constexpr int kGDS = 80;      // LDS floats per delta2 pixel (64 channels + pad)
 constexpr int kBandPx = 64;   // output pixels per band (16 quads)
@@ -1227,7 +1197,6 @@ __global__ __launch_bounds__(512, 1) void wgrad2_kernel(const float* __restrict_
   const int lane = lane_id(), wave = wave_id(), i = lane & 15, gq = lane >> 4;
   const int ct = wave & 1, nt = wave >> 1;
   int cq = blockIdx.x % NCQ, grp = blockIdx.x / NCQ;
-#if SRCNN_WG2_XCD
   if (gridDim.x % (8 * NCQ) == 0) {
     // blocks go round-robin over the 8 XCDs: blocks x, x + 8, ... share an
     // XCD, so a group's NCQ channel quarters are put there and read each
@@ -1236,7 +1205,6 @@ __global__ __launch_bounds__(512, 1) void wgrad2_kernel(const float* __restrict_
     cq = j % NCQ;
     grp = blockIdx.x % 8 + 8 * (j / NCQ);
   }
-#endif
   const bool gbw = cq == 0 && ct == 0;
   f32x4 acc[FF];
 #pragma unroll
@@ -1269,7 +1237,6 @@ __global__ __launch_bounds__(512, 1) void wgrad2_kernel(const float* __restrict_
     const int dslots = (kBandPx + 4) * 20;
     const float* dsrc = D2 + ((size_t)s * g.h2 * g.w2 + (size_t)y0 * g.w2 + x0) * COUT;
     int k0 = 0;  // first 64-slot DMA group of the A1 image that comes from HBM
-#if SRCNN_WG2_HALO
     if (g.nbx == 1 && b > 0 && prev) {
       // the band's first F - 1 A1 rows are the previous band's last F - 1 rows
       // (that band is full, rows = g.rows), already in LDS: copied LDS -> LDS in
@@ -1279,7 +1246,6 @@ __global__ __launch_bounds__(512, 1) void wgrad2_kernel(const float* __restrict_
       float4* dst = reinterpret_cast<float4*>(buf);
       for (int e = threadIdx.x; e < k0 * 64; e += 512) dst[e] = src[e];
     }
-#endif
     if (g.nbx == 1) {  // full-width bands: the band's rows are contiguous in HBM
       for (int k = k0 + wave; k * 64 < aslots; k += 8) {
         const int slot = k * 64 + lane, pix = slot / 12, q = slot - 12 * pix;

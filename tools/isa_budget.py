@@ -1,6 +1,6 @@
 """Issue-slot accounting of a kernel's innermost hot loop from its gfx950 ISA.
 
-    python tools/isa_budget.py <file.s> <kernel-name-substring> [--mfma-cycles 32]
+    python tools/isa_budget.py <file.s> <kernel-name-substring>
 
 Builds the assembly of a source with
     hipcc --offload-arch=gfx950 -O3 ... --cuda-device-only -S -o file.s
@@ -19,6 +19,24 @@ from collections import Counter, OrderedDict
 # 32 cycles when independent; 32x32x2 f32 every 64)
 MFMA_CYCLES = {"v_mfma_f32_16x16x4_f32": 32, "v_mfma_f32_16x16x4f32": 32,
                "v_mfma_f32_32x32x2_f32": 64, "v_mfma_f32_32x32x2f32": 64}
+
+
+# per-wave ISSUE cost of one instruction (cycles), MI355X_MICROARCH.md
+# constants table, row 'vector-instruction ISSUE cost' and the LDS-DMA row:
+# an MFMA holds its SIMD's vector issue for 8 cycles (measured for the bf16
+# forms; assumed here for the f32 ones), a plain VALU op 4, a transcendental
+# 8, an LDS-DMA piece ~60 among MFMAs; every other instruction is charged one
+# issue slot (4).
+ISSUE = {"mfma": 8, "valu": 4, "vmem_dma": 60}
+TRANSCENDENTAL = ("v_exp", "v_log", "v_rcp", "v_rsq", "v_sqrt", "v_sin", "v_cos")
+
+
+def issue_cost(kind, op):
+    if kind == "valu" and op.startswith(TRANSCENDENTAL):
+        return 8
+    if kind == "nop":
+        return 4 if op.startswith("s_nop") else 0
+    return ISSUE.get(kind, 4)
 
 
 def classify(op):
@@ -57,9 +75,6 @@ def kernel_lines(path, name):
     lines = open(path).read().split("\n")
     start = None
     for i, ln in enumerate(lines):
-        if ln.startswith("_Z") and ln.split(":")[0].find(name) >= 0 and ln.rstrip().endswith(
-                ln.split(":")[0] + ":") is False:
-            pass
         if re.match(r"^_Z\S*%s\S*:" % re.escape(name), ln):
             start = i
             break
@@ -106,11 +121,12 @@ def main():
             continue
         seen.add((a, z))
         c = Counter()
-        mcyc = 0
+        mcyc = icyc = 0
         for b in order[a:z + 1]:
             for op, s in blocks[b]:
                 k = classify(op)
                 c[k] += 1
+                icyc += issue_cost(k, op)
                 if k == "mfma":
                     mcyc += MFMA_CYCLES.get(op, 32)
         if c["mfma"] == 0:
@@ -118,7 +134,8 @@ def main():
         non_mfma = sum(v for k, v in c.items() if k not in ("mfma", "nop"))
         print("loop %s..%s (%d blocks): %s" % (order[a], order[z], z - a + 1, dict(sorted(c.items()))))
         print("   MFMA %d = %d matrix-pipe cycles; other issued instructions %d "
-              "(%.2f per MFMA)" % (c["mfma"], mcyc, non_mfma, non_mfma / c["mfma"]))
+              "(%.2f per MFMA); one wave's issue time %d cycles = %.2f of its matrix-pipe time"
+              % (c["mfma"], mcyc, non_mfma, non_mfma / c["mfma"], icyc, icyc / mcyc))
 
 
 if __name__ == "__main__":
