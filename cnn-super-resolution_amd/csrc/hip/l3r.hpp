@@ -425,6 +425,7 @@ __global__ __launch_bounds__(kL3RThreads, 4) void l3r_delta_kernel(  // two 8-wa
           // lane's two quads, read back as whole rows
 #pragma unroll
           for (int t = 0; t < NT; t++) *reinterpret_cast<f32x4*>(scw + srw + 16 * t) = acc[t];
+          __builtin_amdgcn_wave_barrier();  // (cross-lane read-back: no compiler motion across)
           const f32x4 sa = *reinterpret_cast<const f32x4*>(scw + srr);
           const f32x4 sb = *reinterpret_cast<const f32x4*>(scw + srr + 8 * kL3RScS);
           int l_ = lane;
@@ -441,6 +442,7 @@ __global__ __launch_bounds__(kL3RThreads, 4) void l3r_delta_kernel(  // two 8-wa
 #pragma unroll
           for (int i = 0; i < 4; i++)
             scw[sco_w + (16 * h + i) * kL3RScS] = a2r[j][h][i];
+        __builtin_amdgcn_wave_barrier();  // (cross-lane read-back below)
         float ag[4][TT];
 #pragma unroll
         for (int s = 0; s < 4; s++)

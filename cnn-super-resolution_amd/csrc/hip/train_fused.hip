@@ -323,6 +323,9 @@ __global__ __launch_bounds__(256, 2) void l12_fwd_kernel(
           for (int e = 0; e < 4; e++) v_[e] = fmaxf(acc2[4 * m + e], 0.0f);
           *reinterpret_cast<f32x4*>(sc + li * kL12A2S + 8 * m + 4 * h) = v_;
         }
+        // other lanes' values are read back: no compiler motion across this
+        // point (the wave's LDS operations themselves complete in order)
+        __builtin_amdgcn_wave_barrier();
 #pragma unroll
         for (int q = 0; q < 4; q++) {
           const f32x4 v_ = *reinterpret_cast<const f32x4*>(sc + (8 * q + (lane >> 3)) * kL12A2S + 4 * (lane & 7));
@@ -949,9 +952,9 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   const size_t lds3 = l3split ? L3RLds<F3, kL3RUnitsHalf, true>(ow, oh).bytes()
                       : l3r   ? L3RLds<F3>(ow, oh).bytes()
                               : l3_lds_bytes<N2, F3>(ow, oh);
-  // (n2 = 32: l3r takes every tile l3_delta's two LDS images would)
+  // (n2 = 32 tiles past l3r's 512 outputs, e.g. f3 = 3 on 33x33: l3_delta)
   const bool l3_fused =
-      l3r || (N2 != 32 && lds3 <= 160 * 1024 && w3 * h3 <= kL3MaxOut &&
+      l3r || (lds3 <= 160 * 1024 && w3 * h3 <= kL3MaxOut &&
               ((ow * oh + 15) / 16 + kL3Threads / 64 - 1) / (kL3Threads / 64) <= L3Lds<N2, F3>::kUnitsPerWave);
   const int g12 = grid_for_batch(batch, kL12Grid);
   // l3r: up to 2 resident blocks per CU; between 256 and 1024 samples keep
@@ -1020,12 +1023,9 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   if (l3_fused) {
     SRCNN_PROFILE("l3_delta_fused", s);
     kernels_note(l3split ? "l3r_delta_split" : l3r ? "l3r_delta" : "l3_delta");
-    int rc;
-    if constexpr (N2 == 32)
-      rc = l3split ? launch_l3r<F3, kL3RUnitsHalf, true>(A2, T, W3, B3, D2, slab3, sqs, A3, lg, g3, lds3, s)
-                   : launch_l3r<F3, kL3RUnits, false>(A2, T, W3, B3, D2, slab3, sqs, A3, lg, g3, lds3, s);
-    else
-      rc = launch_l3<N2, F3>(A2, T, W3, B3, D2, slab3, sqs, A3, lg, g3, lds3, s);
+    int rc = l3split ? launch_l3r<F3, kL3RUnitsHalf, true>(A2, T, W3, B3, D2, slab3, sqs, A3, lg, g3, lds3, s)
+             : l3r   ? launch_l3r<F3, kL3RUnits, false>(A2, T, W3, B3, D2, slab3, sqs, A3, lg, g3, lds3, s)
+                     : launch_l3<N2, F3>(A2, T, W3, B3, D2, slab3, sqs, A3, lg, g3, lds3, s);
     if (rc) return rc;
   } else {
     // ConfigBasedDataPipeline.cpp:200-323 for layer 3 on the op-level kernels
@@ -1093,19 +1093,11 @@ static int preload_one(const srcnn_net* net) {
   if (net->n1 != (uint32_t)N1 || net->n2 != (uint32_t)N2 || net->f1 != (uint32_t)F1 ||
       net->f2 != 1 || net->f3 != (uint32_t)F3)
     return 0;
-  int rc;
-  if constexpr (N2 == 32) {
-    const void* k[] = {(const void*)l12_fwd_kernel<N1, N2, F1>, (const void*)l12_fwd_kernel<N1, N2, F1, true>,
-                       (const void*)d1_grad12_kernel<N1, N2, F1>, (const void*)slab_reduce_kernel,
-                       (const void*)l3r_delta_kernel<F3>, (const void*)l3r_delta_kernel<F3, kL3RUnitsHalf, true>,
-                       (const void*)d1c_grad12_kernel<9>};
-    rc = resolve_kernels(k, N1 == 64 && F1 == 9 ? 7 : 6);
-  } else {
-    const void* k[] = {(const void*)l12_fwd_kernel<N1, N2, F1>, (const void*)l12_fwd_kernel<N1, N2, F1, true>,
-                       (const void*)l3_delta_kernel<N2, F3>, (const void*)d1_grad12_kernel<N1, N2, F1>,
-                       (const void*)slab_reduce_kernel};
-    rc = resolve_kernels(k, 5);
-  }
+  const void* k[] = {(const void*)l12_fwd_kernel<N1, N2, F1>, (const void*)l12_fwd_kernel<N1, N2, F1, true>,
+                     (const void*)l3_delta_kernel<N2, F3>, (const void*)d1_grad12_kernel<N1, N2, F1>,
+                     (const void*)slab_reduce_kernel, (const void*)l3r_delta_kernel<F3>,
+                     (const void*)l3r_delta_kernel<F3, kL3RUnitsHalf, true>, (const void*)d1c_grad12_kernel<9>};
+  const int rc = resolve_kernels(k, N1 == 64 && N2 == 32 && F1 == 9 ? 8 : 7);
   return rc ? rc : 1;
 }
 

@@ -528,8 +528,10 @@ def test_train_step_nonsquare_tiles(S, w, h, batch):
     ("default", 2, 21, 21, "l3r_delta_split"),
     # whole-sample l3r items
     ("default", 1024, 33, 33, "l3r_delta"), ("default", 1537, 33, 33, "l3r_delta"),
-    # n2 = 16: l3_delta; past 640 A2 pixels: the op-level layer-3 kernels
-    ("example", 16, 33, 33, "l3_delta"), ("default", 3, 39, 39, "l3_op_level")])
+    # n2 = 16, and n2 = 32 past l3r's 512 A3 outputs (f3 = 3 on 33x33: 529):
+    # l3_delta; past 640 A2 pixels: the op-level layer-3 kernels
+    ("example", 16, 33, 33, "l3_delta"), ("default_f3", 7, 33, 33, "l3_delta"),
+    ("default", 3, 39, 39, "l3_op_level")])
 def test_train_step_sq_err_and_a3_vs_oracle(S, name, batch, w, h, l3):
     """The fused step's layer-3 kernel -- which one ran is asserted per case
     (srcnn_last_kernels): gradients, squared error and the A3 it leaves in the

@@ -133,6 +133,9 @@ def main():
             continue
         non_mfma = sum(v for k, v in c.items() if k not in ("mfma", "nop"))
         print("loop %s..%s (%d blocks): %s" % (order[a], order[z], z - a + 1, dict(sorted(c.items()))))
+        if "--ops" in sys.argv:
+            ops = Counter(op for b in order[a:z + 1] for op, _ in blocks[b])
+            print("   ops:", ", ".join("%s %d" % kv for kv in ops.most_common(24)))
         print("   MFMA %d = %d matrix-pipe cycles; other issued instructions %d "
               "(%.2f per MFMA); one wave's issue time %d cycles = %.2f of its matrix-pipe time"
               % (c["mfma"], mcyc, non_mfma, non_mfma / c["mfma"], icyc, icyc / mcyc))
