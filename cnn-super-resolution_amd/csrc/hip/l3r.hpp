@@ -32,8 +32,7 @@
 // at f1 = 9); other shapes keep l3_delta_kernel.
 
 constexpr int kL3RThreads = 512;
-constexpr int kL3RUnits = 5;  // 16-pixel units per wave (8 waves: 640 pixels), whole samples
-constexpr int kL3RUnitsHalf = 4;  // half-sample items (<= 512 pixels)
+constexpr int kL3RUnits = 5;  // 16-pixel units per wave (8 waves: 640 pixels)
 constexpr int kL3RTPF = 1;    // L3 outputs per thread (w3 * h3 <= 512 for every A2 tile of <= 640 pixels)
 constexpr int kL3RW3S = 36;   // W3 image row stride (floats): conflict-free 16-B reads
 constexpr int kL3RScS = 36;   // transpose scratch row stride (floats) per channel
@@ -52,9 +51,9 @@ __host__ __device__ constexpr int l3r_tap(int s, int lg) {
 template <int F3>
 constexpr int l3r_kt() { return F3 == 5 ? 7 : F3; }
 
-template <int F3, int kUnits = kL3RUnits, bool kSplit = false>
+template <int F3>
 struct L3RLds {
-  int qreg;   // Q image [16 * 8 * kUnits][F3^2] (every unit slot); aliased by the transpose scratch and the final reduction
+  int qreg;   // Q image [640][F3^2] (every unit slot); aliased by the transpose scratch and the final reduction
   int w3img;  // W3 image [tap][kL3RW3S] (Q's B operand)
   int wdimg;  // W3 image [c][h][lg][4] at row stride kL3RWdS (delta2's A operand; slot s = 4h + i)
   int d3off;  // delta3 grid offset (F3-1) * (w2 + 1)
@@ -65,7 +64,7 @@ struct L3RLds {
     // track of them and wait for every load right after issuing it), so the
     // Q image and the delta3 grid cover all 8 * kL3RUnits units
     (void)h2;
-    constexpr int npad = 16 * 8 * kUnits;
+    constexpr int npad = 16 * 8 * kL3RUnits;
     int r = npad * F3 * F3;
     if (r < 8 * 32 * kL3RScS) r = 8 * 32 * kL3RScS;
     if (r < 2 * 2 * 4 * 64) r = 2 * 2 * 4 * 64;
@@ -75,10 +74,7 @@ struct L3RLds {
     d3off = (F3 - 1) * (w2 + 1);
     nd3 = 4 + ((npad + d3off + 4 + 3) & ~3);
   }
-  // half-sample items: a second delta3 grid holding only the item's OWN
-  // rows (gW3's operand; the first grid also has the halo rows delta2 needs)
-  __host__ __device__ int nd3o() const { return kSplit ? nd3 : 0; }
-  __host__ __device__ size_t bytes() const { return ((size_t)qreg + w3img + wdimg + nd3 + nd3o()) * sizeof(float); }
+  __host__ __device__ size_t bytes() const { return ((size_t)qreg + w3img + wdimg + nd3) * sizeof(float); }
 };
 
 // the shapes l3r takes: two blocks per CU, whole units per wave
@@ -87,25 +83,6 @@ static bool l3r_fits(int w2, int h2, int w3, int h3) {
   const int nunit = (w2 * h2 + 15) / 16;
   return nunit <= 8 * kL3RUnits && w3 * h3 <= kL3RThreads * kL3RTPF &&
          L3RLds<F3>(w2, h2).bytes() <= 80 * 1024;
-}
-
-// Half-sample items (small batches): a sample's layer 3 split by A3 rows at
-// `a` = h2 / 2 into a top item (A3 rows [0, a): A2 rows [0, a + F3 - 1),
-// delta2 rows [0, a)) and a bottom item (A3 rows [a, h3), delta2 rows
-// [a, h2)); the bottom item recomputes A3 / delta3 rows [a - F3 + 1, a) -- the
-// halo its delta2 rows need -- from A2 rows [a - F3 + 1, h2), and counts
-// only its own rows in A3, the squared error, gB3 and gW3.  Each item's A2 is
-// at most 17 rows of 25 (<= 512 pixels), so a batch of B samples is 2B items
-// and a 512-tile shard fills 512 blocks = two per CU.
-template <int F3>
-__host__ __device__ inline int l3r_split_row(int h2) { return h2 / 2; }
-template <int F3>
-static bool l3r_split_fits(int w2, int h2, int w3, int h3) {
-  const int a = l3r_split_row<F3>(h2);
-  if (a < F3 || h3 - a < 1) return false;
-  const int rows = std::max(a + F3 - 1, h2 - (a - F3 + 1));
-  return rows * w2 <= 16 * 8 * kL3RUnitsHalf && (h3 - (a - F3 + 1)) * w3 <= kL3RThreads * kL3RTPF &&
-         L3RLds<F3, kL3RUnitsHalf, true>(w2, h2).bytes() <= 80 * 1024;
 }
 
 // A2 loads and D2 stores with the nontemporal hint (A2 is read once here,
@@ -118,10 +95,7 @@ __device__ __forceinline__ void st_d2(float* p, f32x4 v) {
   __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p));
 }
 
-// kSplit: work item i is half i & 1 (0 top, 1 bottom) of sample i >> 1; the
-// host launches an even grid, so a block's items are all top or all bottom
-// halves and every per-item range below is fixed per block.
-template <int F3, int kUnits = kL3RUnits, bool kSplit = false>
+template <int F3>
 __global__ __launch_bounds__(kL3RThreads, 4) void l3r_delta_kernel(  // two 8-wave blocks per CU (128 VGPRs)
     const float* __restrict__ A2, const float* __restrict__ T, const float* __restrict__ W3,
     const float* __restrict__ B3, float* __restrict__ D2, float* __restrict__ slab3,
@@ -137,38 +111,21 @@ __global__ __launch_bounds__(kL3RThreads, 4) void l3r_delta_kernel(  // two 8-wa
   SRCNN_CLOCK_BEGIN();
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int npx2 = g.w2 * g.h2;
-  const L3RLds<F3, kUnits, kSplit> L(g.w2, g.h2);
+  const L3RLds<F3> L(g.w2, g.h2);
   const int d3off = L.d3off;
   float* qs = smem;                        // Q[q][tap]
   float* w3s = smem + L.qreg;              // W3[tap][c] at row stride kL3RW3S
   float* wds = w3s + L.w3img;              // W3[tap(s, lg)][c] at c * kL3RWdS + 8 lg + s
   float* d3g = wds + L.wdimg + 4;          // delta3 on the A2 grid (l3_delta.hpp)
-  float* d3o = kSplit ? d3g + L.nd3 : d3g; // delta3 of the item's own rows (gW3's operand)
   float* red = smem;                       // end-of-kernel reduction scratch
-  // this block's item ranges (kSplit: the half is the block's parity; whole
-  // samples otherwise), all in pixels / rows of the item's local A2 grid,
-  // whose row 0 is A2 row r0 of the sample:
-  //   q0    first A2 pixel of the item (r0 * w2); npq A2 pixels loaded
-  //   c0    first A3 row computed (= r0); nrow rows computed, own0 of them halo
-  //   dlo, dhi  local pixel range whose delta2 the item stores
-  const int half = kSplit ? (int)(blockIdx.x & 1) : 0;
-  const int srow = kSplit ? l3r_split_row<F3>(g.h2) : 0;
-  const int r0 = kSplit && half ? srow - (F3 - 1) : 0;
-  const int q0 = r0 * g.w2;
-  const int npq = kSplit ? (half ? npx2 - q0 : (srow + F3 - 1) * g.w2) : npx2;
-  const int nrow = kSplit ? (half ? g.h3 - r0 : srow) : g.h3;
-  const int own0 = kSplit && half ? F3 - 1 : 0;
-  const int dlo = own0 * g.w2, dhi = kSplit && !half ? srow * g.w2 : npq;
-  const int nitems = kSplit ? 2 * g.batch : g.batch;
 
   const int tid = threadIdx.x;
   const int lane = mfma::lane_id(), wave = mfma::wave_id();
   const int lq = lane & 15, lg = lane >> 4;
   const int pad = (g.W - g.w3) / 2;  // last_layer_delta.cl:25
   const int nout = g.w3 * g.h3;
-  const int nloc = nrow * g.w3;      // A3 outputs computed per item
 
-  for (int i = tid - 4; i < L.nd3 - 4 + L.nd3o(); i += kL3RThreads) d3g[i] = 0.0f;
+  for (int i = tid - 4; i < L.nd3 - 4; i += kL3RThreads) d3g[i] = 0.0f;
   for (int i = tid; i < K3 * N2; i += kL3RThreads) w3s[(i / N2) * kL3RW3S + i % N2] = W3[i];
   for (int i = tid; i < 32 * 32; i += kL3RThreads) {
     const int c = i >> 5, gs = i & 31, tap = l3r_tap<F3>(gs & 7, gs >> 3);
@@ -231,7 +188,7 @@ __global__ __launch_bounds__(kL3RThreads, 4) void l3r_delta_kernel(  // two 8-wa
   // their delta2 is not stored, and their delta3 windows lie past every
   // written delta3 (index >= npx2 in the zeroed grid), so they add exactly 0
   // to gW3
-  f32x4 a2r[kUnits][2];
+  f32x4 a2r[kL3RUnits][2];
   // (addresses: a wave-uniform base + one 32-bit lane offset, re-formed at
   // each use; precomputed 64-bit pointers per unit cost registers)
   // (A2 loads / D2 stores: pixel lq & 7, quad lg (lq < 8) or 4 + lg of the row)
@@ -244,10 +201,10 @@ __global__ __launch_bounds__(kL3RThreads, 4) void l3r_delta_kernel(  // two 8-wa
     asm volatile("" : "+v"(l_));                                                        \
     const int lo_ = ((l_ & 7) * N2 + 4 * ((l_ >> 4) + 4 * ((l_ >> 3) & 1)));            \
     const int pa_ = 16 * (wave + nwaves * (J)) + (l_ & 7);                              \
-    const float* b_ = A2 + ((size_t)(SAMPLE)*npx2 + q0) * N2;                           \
+    const float* b_ = A2 + (size_t)(SAMPLE)*npx2 * N2;                                  \
     const unsigned w_ = 16 * (wave + nwaves * (J)) * N2 + lo_;                          \
-    const unsigned oa_ = pa_ < npq ? w_ : lo_; /* else pixel lq & 7 of the item */      \
-    const unsigned ob_ = pa_ + 8 < npq ? w_ + 8 * N2 : lo_;                             \
+    const unsigned oa_ = pa_ < npx2 ? w_ : lo_; /* else pixel lq & 7 of the sample */   \
+    const unsigned ob_ = pa_ + 8 < npx2 ? w_ + 8 * N2 : lo_;                            \
     a2r[J][0] = ld_a2(b_ + oa_);                                                        \
     a2r[J][1] = ld_a2(b_ + ob_);                                                        \
   } while (0)
@@ -272,7 +229,7 @@ __global__ __launch_bounds__(kL3RThreads, 4) void l3r_delta_kernel(  // two 8-wa
   for (int k = 0; k < kL3RTPF; k++) {
     const int t_ = tid + k * kL3RThreads;
     const int y_ = t_ / g.w3, x_ = t_ - y_ * g.w3;
-    tof[k] = t_ < nloc ? (r0 + y_ + pad) * g.W + x_ + pad : -1;
+    tof[k] = t_ < nout ? (y_ + pad) * g.W + x_ + pad : -1;
   }
   float tpf[kL3RTPF];
 #define SRCNN_L3R_T_PREFETCH(SAMPLE)                                                   \
@@ -284,35 +241,32 @@ __global__ __launch_bounds__(kL3RThreads, 4) void l3r_delta_kernel(  // two 8-wa
     }                                                                                  \
   } while (0)
 
-  // item -> sample (kSplit: two items per sample, the halves of a block
-  // share its parity)
-  auto item_sample = [&](int it) { return l3_order(kSplit ? it >> 1 : it, g.batch); };
-  if ((int)blockIdx.x < nitems) {
-    const int s0 = item_sample(blockIdx.x);
+  if ((int)blockIdx.x < g.batch) {
+    const int s0 = l3_order(blockIdx.x, g.batch);
 #pragma unroll
-    for (int j = 0; j < kUnits; j++) SRCNN_L3R_LOAD(j, s0);
+    for (int j = 0; j < kL3RUnits; j++) SRCNN_L3R_LOAD(j, s0);
     SRCNN_L3R_T_PREFETCH(s0);
   }
 
-  for (int sample = blockIdx.x; sample < nitems; sample += gridDim.x) {
+  for (int sample = blockIdx.x; sample < g.batch; sample += gridDim.x) {
     // the previous sample's readers of the transpose scratch (= Q image) and
     // of the delta3 grid are done; a bare barrier: the next sample's A2
     // loads and this sample's D2 stores stay in flight
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    const int smp = item_sample(sample);
+    const int smp = l3_order(sample, g.batch);
     float tcur[kL3RTPF];
 #pragma unroll
     for (int k = 0; k < kL3RTPF; k++) tcur[k] = tpf[k];
     const int next = sample + (int)gridDim.x;
-    const bool has_next = next < nitems;
-    const int nsmp = has_next ? item_sample(next) : smp;
+    const bool has_next = next < g.batch;
+    const int nsmp = has_next ? l3_order(next, g.batch) : smp;
     SRCNN_L3R_T_PREFETCH(nsmp);  // (a harmless re-read without a next sample)
 
     // ---- Q = A2 . W3^T per 16-pixel unit, A operand from registers ----
 #pragma unroll
-    for (int j = 0; j < kUnits; j++) {
+    for (int j = 0; j < kL3RUnits; j++) {
       __builtin_amdgcn_sched_barrier(0);  // no operand motion across units (registers)
       const int u = wave + nwaves * j;
       {  // every slot, also past the sample's units (zero A2, stores masked)
@@ -352,8 +306,8 @@ __global__ __launch_bounds__(kL3RThreads, 4) void l3r_delta_kernel(  // two 8-wa
 #pragma unroll
     for (int k = 0; k < kL3RTPF; k++) {
       const int t = tid + k * kL3RThreads;
-      if (t < nloc) {
-        const int y = t / g.w3, x = t - y * g.w3;  // (local row)
+      if (t < nout) {
+        const int y = t / g.w3, x = t - y * g.w3;
         const float* qrow = qs + (y * g.w2 + x) * K3;
         float acc = 0.0f;
 #pragma unroll
@@ -361,15 +315,12 @@ __global__ __launch_bounds__(kL3RThreads, 4) void l3r_delta_kernel(  // two 8-wa
 #pragma unroll
           for (int dx = 0; dx < F3; dx++) acc += qrow[(dy * g.w2 + dx) * K3 + dy * F3 + dx];
         const float a3 = acc + b3;
+        A3out[(size_t)smp * nout + t] = a3;
         const float diff = a3 - tcur[k];
         const float d3 = diff * (a3 > 0.0f ? 1.0f : 0.0f);
         d3g[y * g.w2 + x + d3off] = d3;
-        if (y >= own0) {  // (kSplit: the bottom item's halo rows only feed delta2)
-          A3out[(size_t)smp * nout + r0 * g.w3 + t] = a3;
-          if (kSplit) d3o[y * g.w2 + x + d3off] = d3;
-          gb3 += d3;
-          sq += diff * diff;
-        }
+        gb3 += d3;
+        sq += diff * diff;
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -382,9 +333,9 @@ __global__ __launch_bounds__(kL3RThreads, 4) void l3r_delta_kernel(  // two 8-wa
     // delta2 runs transposed (M = channels, N = pixels): C register i of lane
     // (lq, lg) in tile t is delta2[u0 + lq][16t + 4lg + i], whose relu' mask
     // is a2r[j][t][i].  Then this unit's registers take the next sample's A2.
-    float* d2s = D2 + ((size_t)smp * npx2 + q0 + 16 * wave) * N2;
+    float* d2s = D2 + ((size_t)smp * npx2 + 16 * wave) * N2;
 #pragma unroll
-    for (int j = 0; j < kUnits; j++) {
+    for (int j = 0; j < kL3RUnits; j++) {
       __builtin_amdgcn_sched_barrier(0);  // no operand motion across units (registers)
       const int u = wave + nwaves * j;
       {  // every slot, also past the sample's units (zero A2, stores masked)
@@ -431,9 +382,8 @@ __global__ __launch_bounds__(kL3RThreads, 4) void l3r_delta_kernel(  // two 8-wa
           int l_ = lane;
           asm volatile("" : "+v"(l_));  // (formed at the store, not held across the loop)
           const unsigned o_ = (l_ & 7) * N2 + 4 * ((l_ >> 4) + 4 * ((l_ >> 3) & 1)) + 16 * nwaves * N2 * j;
-          const int pd_ = u0 + (lq & 7);
-          if (pd_ >= dlo && pd_ < dhi) st_d2(d2s + o_, sa);
-          if (pd_ + 8 >= dlo && pd_ + 8 < dhi) st_d2(d2s + o_ + 8 * N2, sb);
+          if (u0 + (lq & 7) < npx2) st_d2(d2s + o_, sa);
+          if (u0 + 8 + (lq & 7) < npx2) st_d2(d2s + o_ + 8 * N2, sb);
         }
         __builtin_amdgcn_sched_barrier(0);
         // gW3's B operand A2[u0 + 4lg + s][16t + lq] through the scratch
@@ -447,7 +397,7 @@ __global__ __launch_bounds__(kL3RThreads, 4) void l3r_delta_kernel(  // two 8-wa
 #pragma unroll
         for (int s = 0; s < 4; s++)
 #pragma unroll
-          for (int t3 = 0; t3 < TT; t3++) ag[s][t3] = d3o[agb[t3] + 128 * j + s];
+          for (int t3 = 0; t3 < TT; t3++) ag[s][t3] = d3g[agb[t3] + 128 * j + s];
         f32x4 bg[NT];
 #pragma unroll
         for (int t = 0; t < NT; t++) bg[t] = *reinterpret_cast<const f32x4*>(scw + wqo + 16 * t * kL3RScS);

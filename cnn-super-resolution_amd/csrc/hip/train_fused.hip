@@ -889,29 +889,19 @@ struct Net {
 
 static int grid_for_batch(uint32_t batch, int cap) { return (int)std::min<uint32_t>(batch, cap); }
 
-template <int F3, int kUnits, bool kSplit>
+template <int F3>
 static int launch_l3r(const float* A2, const float* T, const float* W3, const float* B3, float* D2,
                       float* slab3, float* sqs, float* A3, const L3Geom& lg, int grid, size_t lds,
                       hipStream_t s) {
   // 70 KB exceeds the 64 KiB default dynamic LDS (set per launch: see launch_l3)
-  hipError_t e = hipFuncSetAttribute((const void*)l3r_delta_kernel<F3, kUnits, kSplit>,
+  hipError_t e = hipFuncSetAttribute((const void*)l3r_delta_kernel<F3>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
   if (e != hipSuccess)
     return fail(SRCNN_ERR_HIP, "hipFuncSetAttribute(l3r_delta): %s", hipGetErrorString(e));
-  hipLaunchKernelGGL((l3r_delta_kernel<F3, kUnits, kSplit>), dim3(grid), dim3(kL3RThreads), lds, s, A2, T,
-                     W3, B3, D2, slab3, sqs, A3, lg);
+  hipLaunchKernelGGL((l3r_delta_kernel<F3>), dim3(grid), dim3(kL3RThreads), lds, s, A2, T, W3, B3,
+                     D2, slab3, sqs, A3, lg);
   SRCNN_LAUNCH_TRY();
   return SRCNN_OK;
-}
-
-// below this batch, l3r runs half-sample items (l3r.hpp: l3r_split_row), so
-// that a small shard still fills two blocks per CU
-static int l3r_split_below() {
-  static const int v = [] {
-    const char* e = getenv("SRCNN_L3R_SPLIT_BELOW");
-    return e ? atoi(e) : 1024;
-  }();
-  return v;
 }
 
 template <int N2, int F3>
@@ -948,10 +938,7 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   // (ops_fast.hip: L3 forward, last delta, delta2, gW3 over HWC A2 / A3 / D3).
   // n2 = 32: l3r (A2 in registers, two blocks per CU) where the tile fits it
   const bool l3r = N2 == 32 && l3r_fits<F3>(ow, oh, w3, h3);
-  const bool l3split = l3r && (int)batch < l3r_split_below() && l3r_split_fits<F3>(ow, oh, w3, h3);
-  const size_t lds3 = l3split ? L3RLds<F3, kL3RUnitsHalf, true>(ow, oh).bytes()
-                      : l3r   ? L3RLds<F3>(ow, oh).bytes()
-                              : l3_lds_bytes<N2, F3>(ow, oh);
+  const size_t lds3 = l3r ? L3RLds<F3>(ow, oh).bytes() : l3_lds_bytes<N2, F3>(ow, oh);
   // (n2 = 32 tiles past l3r's 512 outputs, e.g. f3 = 3 on 33x33: l3_delta)
   const bool l3_fused =
       l3r || (lds3 <= 160 * 1024 && w3 * h3 <= kL3MaxOut &&
@@ -962,11 +949,8 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   // one's delta2 phase (512 tiles: l3 0.0306 -> 0.0295 ms; at batch 4096 a
   // 256-block grid is slower, 0.155 -> 0.167 ms; profiles/r04_ab_l3rgrid)
   const int b3 = (int)batch;
-  // half-sample items: 2 * batch of them, an even grid (a block's items are
-  // all top or all bottom halves)
-  const int g3 = l3split ? std::min(kL3RGrid, 2 * b3)
-                 : l3r   ? std::min(kL3RGrid, std::max(std::min(b3, 256), (b3 + 1) / 2))
-                         : grid_for_batch(batch, 256);
+  const int g3 = l3r ? std::min(kL3RGrid, std::max(std::min(b3, 256), (b3 + 1) / 2))
+                     : grid_for_batch(batch, 256);
   const bool kD1c = N1 == 64 && N2 == 32 && F1 == 9 && d1c_fits(w, h);
   // d1c below kD1cGrid samples: each sample's chunks split into `parts`
   // ranges (work items), so the grid still fills every CU's 4 block slots
@@ -1022,10 +1006,9 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   L3Geom lg{(int)w, (int)h, ow, oh, w3, h3, (int)batch};
   if (l3_fused) {
     SRCNN_PROFILE("l3_delta_fused", s);
-    kernels_note(l3split ? "l3r_delta_split" : l3r ? "l3r_delta" : "l3_delta");
-    int rc = l3split ? launch_l3r<F3, kL3RUnitsHalf, true>(A2, T, W3, B3, D2, slab3, sqs, A3, lg, g3, lds3, s)
-             : l3r   ? launch_l3r<F3, kL3RUnits, false>(A2, T, W3, B3, D2, slab3, sqs, A3, lg, g3, lds3, s)
-                     : launch_l3<N2, F3>(A2, T, W3, B3, D2, slab3, sqs, A3, lg, g3, lds3, s);
+    kernels_note(l3r ? "l3r_delta" : "l3_delta");
+    int rc = l3r ? launch_l3r<F3>(A2, T, W3, B3, D2, slab3, sqs, A3, lg, g3, lds3, s)
+                 : launch_l3<N2, F3>(A2, T, W3, B3, D2, slab3, sqs, A3, lg, g3, lds3, s);
     if (rc) return rc;
   } else {
     // ConfigBasedDataPipeline.cpp:200-323 for layer 3 on the op-level kernels
@@ -1096,8 +1079,8 @@ static int preload_one(const srcnn_net* net) {
   const void* k[] = {(const void*)l12_fwd_kernel<N1, N2, F1>, (const void*)l12_fwd_kernel<N1, N2, F1, true>,
                      (const void*)l3_delta_kernel<N2, F3>, (const void*)d1_grad12_kernel<N1, N2, F1>,
                      (const void*)slab_reduce_kernel, (const void*)l3r_delta_kernel<F3>,
-                     (const void*)l3r_delta_kernel<F3, kL3RUnitsHalf, true>, (const void*)d1c_grad12_kernel<9>};
-  const int rc = resolve_kernels(k, N1 == 64 && N2 == 32 && F1 == 9 ? 8 : 7);
+                     (const void*)d1c_grad12_kernel<9>};
+  const int rc = resolve_kernels(k, N1 == 64 && N2 == 32 && F1 == 9 ? 7 : 6);
   return rc ? rc : 1;
 }
 

@@ -263,7 +263,7 @@ SRCNN_API int srcnn_get_path(void);
 SRCNN_API const char* srcnn_last_path(void);
 /* The kernels, by variant, that this thread's most recent training call
  * (srcnn_train_fwd_bwd / _step / _lazy) launched, comma-separated, e.g.
- * "l12_fwd,l3r_delta_split,d1c_grad12,slab_reduce" -- so that a test can
+ * "l12_fwd,l3r_delta,d1c_grad12,slab_reduce" -- so that a test can
  * assert which specialisation served a shape.  "" before any such call. */
 SRCNN_API const char* srcnn_last_kernels(void);
 

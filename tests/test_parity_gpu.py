@@ -521,13 +521,10 @@ def test_train_step_nonsquare_tiles(S, w, h, batch):
 
 
 @pytest.mark.parametrize("name,batch,w,h,l3", [
-    # below 1024 samples l3r runs half-sample items (top / bottom A3 rows, the
-    # bottom item recomputing the 4-row delta3 halo its delta2 rows need)
-    ("default", 16, 33, 33, "l3r_delta_split"), ("default", 512, 33, 33, "l3r_delta_split"),
-    ("default", 257, 33, 33, "l3r_delta_split"), ("default", 7, 35, 31, "l3r_delta_split"),
-    ("default", 2, 21, 21, "l3r_delta_split"),
-    # whole-sample l3r items
-    ("default", 1024, 33, 33, "l3r_delta"), ("default", 1537, 33, 33, "l3r_delta"),
+    # l3r: one sample (256-1024 samples: two) per block
+    ("default", 16, 33, 33, "l3r_delta"), ("default", 512, 33, 33, "l3r_delta"),
+    ("default", 257, 33, 33, "l3r_delta"), ("default", 7, 35, 31, "l3r_delta"),
+    ("default", 2, 21, 21, "l3r_delta"), ("default", 1537, 33, 33, "l3r_delta"),
     # n2 = 16, and n2 = 32 past l3r's 512 A3 outputs (f3 = 3 on 33x33: 529):
     # l3_delta; past 640 A2 pixels: the op-level layer-3 kernels
     ("example", 16, 33, 33, "l3_delta"), ("default_f3", 7, 33, 33, "l3_delta"),
