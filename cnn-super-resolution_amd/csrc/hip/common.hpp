@@ -41,6 +41,8 @@ inline uint32_t grid_for(size_t total, uint32_t block, uint32_t cap = 1u << 20) 
 
 // kernel-path selection (srcnn_set_path): 0 auto, 1 generic only
 extern int g_path;
+// matrix-core arithmetic (srcnn_set_arith): 0 split bf16, 1 fp32 MFMA only
+extern int g_arith;
 
 // Per-launch hipEvent bracketing for srcnn_profile_* (reference profile
 // mode, src/opencl/Kernel.cpp:108-116).  A no-op unless profiling is on.

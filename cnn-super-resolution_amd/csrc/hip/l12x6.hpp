@@ -1,0 +1,332 @@
+// l12x6.hpp -- kernel 1 of the fused step (L1 + L2 forward) for the reference
+// default net (n1 = 64, n2 = 32, f1 = 9) with its products on the bf16 matrix
+// cores in exact-split form.  Included by train_fused.hip inside namespace
+// srcnn::fused; same outputs (blocked A1, A2 rows) and the same mathematics as
+// l12_fwd_kernel (layer_uber_kernel.cl:36-96 for layers 1 and 2).
+//
+// Split products ("x6", split.hpp): every fp32 operand is the sum of three
+// bf16 parts (round-to-nearest residuals, exact to 2^-27 relative), and a
+// product a . b is formed from the six part products whose order is at most
+// 2^-16; the dropped ones are below 2^-26 relative, under the 2^-24 rounding
+// of an fp32 product.  v_mfma_f32_32x32x16_bf16 forms exact part products
+// and sums them in fp32, so a 32x32x16 block costs 6 x 32 cycles against
+// 8 x 64 for v_mfma_f32_32x32x2_f32, at fp32 accuracy (profiles/r05_x6:
+// normwise error against an fp64 product 1.45e-7 vs 1.79e-7 for the fp32
+// MFMA chain at K = 96).
+//
+// Layer 1, transposed as in l12_fwd (rows = channels, cols = the chunk's 32
+// pixels), K = taps: 80 taps in 5 bf16 k-steps of 16 slots, tap (8, 8) and
+// the bias in one fp32 32x32x2 MFMA that starts the accumulator.  Slot
+// 8h + j of k-step s (lane half h, element j) is
+//   group g = 2s + h <= 8: tap (dy = g, dx = j)       (a row run of X)
+//   group g = 9:           tap (dy = j, dx = 8)       (column 8)
+// so a lane's 8 B-operand values are 8 consecutive X pixels of one row for
+// k-steps 0-3: four dwords of the PAIR image R (dword i = parts of x_i and
+// x_{i+1}), i.e. two ds_read2_b32 per part.  K-step 4 (row 8 / column 8)
+// reads the fp32 tile and splits in registers.
+// Layer 2: the L1 accumulator after ReLU is split in registers (k-step m:
+// registers 8(m&1) .. +7 of tile m>>1, the channel order of mfma.hpp's crow)
+// against W2 split images; B2 starts the accumulator as in l12_fwd.
+// W1 and W2 live in LDS as split operand images (one ds_read_b128 per part
+// and tile), formed once per block, with the lazy update folded in.
+using mfma::bf16x8;
+using mfma::mma_x6;
+using mfma::relu1;
+using mfma::split3;
+using mfma::split8;
+using mfma::u32x4;
+
+constexpr int kX6KS = 5;                  // bf16 k-steps of layer 1
+constexpr int kX6W1 = kX6KS * 2 * 3 * 512;  // W1 image, bf16: [s][t][part][lane][8]
+constexpr int kX6W2 = 4 * 3 * 512;          // W2 image, bf16: [m][part][lane][8]
+
+struct X6Lds {
+  int r, xs, a2sc, bytes;  // byte offsets of the pair images, the fp32 tile, the A2 scratch
+  __host__ __device__ X6Lds(int w, int h) {
+    const int n = w * h;
+    const int base = (kX6W1 + kX6W2) * 2 + (128 + 32) * 4;
+    r = base;
+    xs = r + 3 * (n + 1) * 4;
+    a2sc = (xs + n * 4 + 15) & ~15;
+    bytes = a2sc + 4 * 32 * kL12A2S * 4;
+  }
+};
+
+inline bool l12x6_fits(int w, int h) {
+  return w * h <= kXsMax && X6Lds(w, h).bytes <= 80 * 1024;
+}
+
+template <bool kLazy>
+__global__ __launch_bounds__(256, 2) void l12x6_fwd_kernel(const float* __restrict__ X,
+                                                            const float* __restrict__ W1,
+                                                            const float* __restrict__ B1,
+                                                            const float* __restrict__ W2,
+                                                            const float* __restrict__ B2,
+                                                            float* __restrict__ A1,
+                                                            float* __restrict__ A2, Geom g, LazyUpdate lz) {
+  constexpr int N1 = 64, N2 = 32, F1 = 9, NT1 = 2;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const X6Lds L(g.W, g.H);
+  __bf16* const w1i = reinterpret_cast<__bf16*>(smem);
+  __bf16* const w2i = w1i + kX6W1;
+  float* const a88s = reinterpret_cast<float*>(w2i + kX6W2);  // [W1 tap 80 | B1]
+  float* const b2i = a88s + 128;                              // [2][16]
+  uint32_t* const rimg = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(smem) + L.r);
+  float* const xs = reinterpret_cast<float*>(reinterpret_cast<char*>(smem) + L.xs);
+  float* const a2sc = reinterpret_cast<float*>(reinterpret_cast<char*>(smem) + L.a2sc);
+
+  SRCNN_CLOCK_BEGIN();
+  const int lane = mfma::lane_id(), wave = mfma::wave_id();
+  const int h = lane >> 5, li = lane & 31;
+  const int W = g.W, xn = g.W * g.H;
+  const int npx = g.ow * g.oh, nch = (npx + 31) / 32;
+  const int rn = xn + 1;  // pair-image dwords per part
+
+  float xr[kL12Regs];
+  auto xload = [&](int smp) {
+    const float* src = X + (size_t)smp * xn;
+#pragma unroll
+    for (int k = 0; k < kL12Regs; k++) {
+      const int i = threadIdx.x + 256 * k;
+      xr[k] = i < xn ? src[i] : 0.0f;
+    }
+  };
+  if ((int)blockIdx.x < g.batch) xload(blockIdx.x);
+
+  // ---- split operand images of W1 / W2 (with the pending update folded in) ----
+  if constexpr (kLazy) lazy_write_slice(lz);
+  auto prm = [&](int seg, int i) -> float {
+    if constexpr (kLazy) return lazy_param(lz, seg, i);
+    return (seg == 0 ? W1 : seg == 1 ? B1 : seg == 2 ? W2 : B2)[i];
+  };
+  {
+    // W1: element e = (s, t, lane, j); every tap but (8, 8) exactly once
+    constexpr int kN = kX6KS * 2 * 64 * 8, kIt = kN / 256;
+    float v[kIt];
+#pragma unroll
+    for (int k = 0; k < kIt; k++) {
+      const int e = threadIdx.x + 256 * k;
+      const int j = e & 7, L_ = (e >> 3) & 63, t = (e >> 9) & 1, s = e >> 10;
+      const int gg = 2 * s + (L_ >> 5);
+      const int tap = gg <= 8 ? gg * F1 + j : j * F1 + 8;
+      v[k] = prm(0, tap * N1 + 32 * t + (L_ & 31));
+    }
+#pragma unroll
+    for (int k = 0; k < kIt; k++) {
+      const int e = threadIdx.x + 256 * k;
+      const int j = e & 7, L_ = (e >> 3) & 63, t = (e >> 9) & 1, s = e >> 10;
+      __bf16 p[3];
+      split3(v[k], p[0], p[1], p[2]);
+#pragma unroll
+      for (int q = 0; q < 3; q++) w1i[((s * 2 + t) * 3 + q) * 512 + L_ * 8 + j] = p[q];
+    }
+  }
+  {
+    // W2^T as the L2 A operand: k-step m, lane (n, h), element j <-> channel
+    // 32 (m >> 1) + crow(8 (m & 1) + j, h)
+    constexpr int kN = 4 * 64 * 8, kIt = kN / 256;
+    float v[kIt];
+#pragma unroll
+    for (int k = 0; k < kIt; k++) {
+      const int e = threadIdx.x + 256 * k;
+      const int j = e & 7, L_ = (e >> 3) & 63, m = e >> 9;
+      const int c = 32 * (m >> 1) + crow(8 * (m & 1) + j, L_ >> 5);
+      v[k] = prm(2, c * N2 + (L_ & 31));
+    }
+#pragma unroll
+    for (int k = 0; k < kIt; k++) {
+      const int e = threadIdx.x + 256 * k;
+      const int j = e & 7, L_ = (e >> 3) & 63, m = e >> 9;
+      __bf16 p[3];
+      split3(v[k], p[0], p[1], p[2]);
+#pragma unroll
+      for (int q = 0; q < 3; q++) w2i[(m * 3 + q) * 512 + L_ * 8 + j] = p[q];
+    }
+  }
+  if (threadIdx.x < 128)
+    a88s[threadIdx.x] = threadIdx.x < 64 ? prm(0, 80 * N1 + threadIdx.x) : prm(1, threadIdx.x - 64);
+  else if (threadIdx.x < 160) {
+    const int i = threadIdx.x - 128;
+    b2i[i] = prm(3, crow(i & 15, i >> 4));
+  }
+  __syncthreads();
+  // fp32 MFMA operand of tap (8, 8) (half 0) and the bias (half 1)
+  float a88r[NT1];
+#pragma unroll
+  for (int t = 0; t < NT1; t++) a88r[t] = a88s[64 * h + 32 * t + li];
+
+  // ---- software-pipelined stores of the previous chunk (as in l12_fwd) ----
+  constexpr int NST = 4 * NT1 + N2 / 8;
+  f32x16 pa1[NT1], pa2 = zero16();
+#pragma unroll
+  for (int t = 0; t < NT1; t++) pa1[t] = zero16();
+  bool pok = false;
+  float* pa1p = A1;
+  float* pa2p = A2;
+  int pc0 = 0;
+  auto store_prev = [&](int k) {
+    if (pok) {
+      if (k < 4 * NT1) {
+        const int t = k / 4, q = k % 4;
+        f32x4 v_;
+#pragma unroll
+        for (int e = 0; e < 4; e++) v_[e] = pa1[t][4 * q + e];
+        __builtin_nontemporal_store(v_, reinterpret_cast<f32x4*>(pa1p + 256 * k));
+      } else {
+        const int q = k - 4 * NT1;
+        if (pc0 + 8 * q + (lane >> 3) < npx) {
+          f32x4 v_;
+#pragma unroll
+          for (int e = 0; e < 4; e++) v_[e] = pa2[4 * q + e];
+          *reinterpret_cast<f32x4*>(pa2p + (8 * q + (lane >> 3)) * N2 + 4 * (lane & 7)) = v_;
+        }
+      }
+    }
+  };
+
+  const uint16_t* const wl1 = reinterpret_cast<const uint16_t*>(w1i) + lane * 8;
+  const uint16_t* const wl2 = reinterpret_cast<const uint16_t*>(w2i) + lane * 8;
+  auto w1op = [&](int s, int t, bf16x8 (&a)[3]) {
+#pragma unroll
+    for (int q = 0; q < 3; q++) a[q] = *reinterpret_cast<const bf16x8*>(wl1 + ((s * 2 + t) * 3 + q) * 512);
+  };
+
+  for (int sample = blockIdx.x; sample < g.batch; sample += gridDim.x) {
+    __syncthreads();  // previous sample's readers are done with the images
+    {
+      uint16_t* const r16 = reinterpret_cast<uint16_t*>(rimg);
+#pragma unroll
+      for (int k = 0; k < kL12Regs; k++) {
+        const int i = threadIdx.x + 256 * k;
+        if (i < xn) {
+          xs[i] = xr[k];
+          __bf16 p[3];
+          split3(xr[k], p[0], p[1], p[2]);
+#pragma unroll
+          for (int q = 0; q < 3; q++) {
+            const uint16_t b = __builtin_bit_cast(uint16_t, p[q]);
+            r16[2 * (q * rn + i)] = b;                  // low half of dword i
+            if (i > 0) r16[2 * (q * rn + i) - 1] = b;   // high half of dword i - 1
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (sample + (int)gridDim.x < g.batch) xload(sample + gridDim.x);
+
+    for (int c = wave; c < nch; c += 4) {
+      const int pl = c * 32 + li;
+      const int pc = min(pl, npx - 1);
+      const int iy = pc / g.ow, ix = pc - iy * g.ow;
+      const int rb = (iy + h) * W + ix;  // row 2s + h of k-steps 0-3
+      // k-step 4: half 0 row 8 (dx 0..7), half 1 column 8 (dy 0..7)
+      const int b4 = h ? iy * W + ix + 8 : (iy + 8) * W + ix, st4 = h ? W : 1;
+
+      f32x16 acc1[NT1];
+      {
+        const float bx = h ? 1.0f : xs[(iy + 8) * W + ix + 8];
+#pragma unroll
+        for (int t = 0; t < NT1; t++) acc1[t] = mma(a88r[t], bx, zero16());
+      }
+      // B operand of k-steps 0-3: rows 2s + h of the pair images
+      auto xop = [&](int s, bf16x8 (&b)[3]) {
+#pragma unroll
+        for (int q = 0; q < 3; q++) {
+          const uint32_t* r = rimg + q * rn + rb + 2 * s * W;
+          u32x4 d;
+          d[0] = r[0];
+          d[1] = r[2];
+          d[2] = r[4];
+          d[3] = r[6];
+          b[q] = __builtin_bit_cast(bf16x8, d);
+        }
+      };
+      // Operand pipeline over the 10 (k-step, tile) groups of 6 MFMAs: the
+      // next group's W1 parts (and at t = 0 the next k-step's X parts) are
+      // read before this group's MFMAs, pinned by sched barriers (left
+      // alone, the scheduler reads each operand just before its MFMA and the
+      // wave waits out the LDS latency every group).  K-step 4's fp32 X
+      // values are read at group 4 and split at group 6.
+      bf16x8 wa[2][3], xb[2][3];
+      float x4[8];
+      xop(0, xb[0]);
+      w1op(0, 0, wa[0]);
+#pragma unroll
+      for (int gi = 0; gi < 2 * kX6KS; gi++) {
+        const int s = gi >> 1, t = gi & 1;
+        if (gi + 1 < 2 * kX6KS) w1op((gi + 1) >> 1, (gi + 1) & 1, wa[(gi + 1) & 1]);
+        if (t == 0 && s + 1 < 4) xop(s + 1, xb[(s + 1) & 1]);
+        if (gi == 4) {
+#pragma unroll
+          for (int j = 0; j < 8; j++) x4[j] = xs[b4 + j * st4];
+        }
+        if (gi == 6) split8(x4, xb[0]);
+        __builtin_amdgcn_sched_barrier(0);
+        acc1[t] = mma_x6(wa[gi & 1], xb[s & 1], acc1[t]);
+        store_prev(gi);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int t = 0; t < NT1; t++)
+#pragma unroll
+        for (int r = 0; r < 16; r++) acc1[t][r] = relu1(acc1[t][r]);
+      f32x16 acc2;
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const f32x4 v_ = *reinterpret_cast<const f32x4*>(&b2i[16 * h + 4 * q]);
+#pragma unroll
+        for (int e = 0; e < 4; e++) acc2[4 * q + e] = v_[e];
+      }
+      // L2: k-step m's A1 parts are split while k-step m - 1's MFMAs run
+      bf16x8 wb[2][3], bb[2][3];
+      auto a1split = [&](int m, bf16x8 (&b)[3]) {
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) v[j] = acc1[m >> 1][8 * (m & 1) + j];
+        split8(v, b);
+      };
+      auto w2op = [&](int m, bf16x8 (&a)[3]) {
+#pragma unroll
+        for (int q = 0; q < 3; q++) a[q] = *reinterpret_cast<const bf16x8*>(wl2 + (m * 3 + q) * 512);
+      };
+      w2op(0, wb[0]);
+      a1split(0, bb[0]);
+#pragma unroll
+      for (int m = 0; m < 4; m++) {
+        if (m + 1 < 4) w2op(m + 1, wb[(m + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+        acc2 = mma_x6(wb[m & 1], bb[m & 1], acc2);
+        if (m + 1 < 4) a1split(m + 1, bb[(m + 1) & 1]);
+        if (m < 2) store_prev(10 + m);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int t = 0; t < NT1; t++) pa1[t] = acc1[t];
+      {
+        float* sc = a2sc + wave * 32 * kL12A2S;
+#pragma unroll
+        for (int m = 0; m < 4; m++) {
+          f32x4 v_;
+#pragma unroll
+          for (int e = 0; e < 4; e++) v_[e] = relu1(acc2[4 * m + e]);
+          *reinterpret_cast<f32x4*>(sc + li * kL12A2S + 8 * m + 4 * h) = v_;
+        }
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const f32x4 v_ = *reinterpret_cast<const f32x4*>(sc + (8 * q + (lane >> 3)) * kL12A2S + 4 * (lane & 7));
+#pragma unroll
+          for (int e = 0; e < 4; e++) pa2[4 * q + e] = v_[e];
+        }
+        pc0 = c * 32;
+      }
+      pok = true;
+      pa1p = A1 + ((size_t)sample * nch + c) * (32 * N1) + 4 * lane;
+      pa2p = A2 + ((size_t)sample * npx + c * 32) * N2;
+    }
+  }
+  // (a sample's last chunk is stored under the next sample's first one)
+#pragma unroll
+  for (int k = 0; k < NST; k++) store_prev(k);
+  SRCNN_CLOCK_END(g_clk, 0);
+}

@@ -24,6 +24,12 @@ static int initial_path() {
   return e && !strcmp(e, "generic") ? 1 : 0;
 }
 int g_path = initial_path();
+// SRCNN_ARITH=f32 starts the library on the fp32-MFMA kernels (srcnn_set_arith)
+static int initial_arith() {
+  const char* e = getenv("SRCNN_ARITH");
+  return e && !strcmp(e, "f32") ? 1 : 0;
+}
+int g_arith = initial_arith();
 
 int fail(int code, const char* fmt, ...) {
   char buf[1024];
@@ -139,6 +145,15 @@ int srcnn_set_path(int path) {
 }
 
 int srcnn_get_path(void) { return srcnn::g_path; }
+
+int srcnn_set_arith(int arith) {
+  SRCNN_REQUIRE(arith == 0 || arith == 1, "srcnn_set_arith: arith must be 0 (split bf16) or 1 (fp32 MFMA), got %d",
+                arith);
+  srcnn::g_arith = arith;
+  return SRCNN_OK;
+}
+
+int srcnn_get_arith(void) { return srcnn::g_arith; }
 
 int srcnn_profile_enable(int on) {
   srcnn::prof::g_enabled = on != 0;

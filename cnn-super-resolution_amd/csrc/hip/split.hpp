@@ -1,0 +1,67 @@
+// split.hpp -- fp32 products on the gfx950 bf16 matrix cores in exact-split
+// form (used by l12x6.hpp).
+//
+// a = a0 + a1 + a2 with a0 = bf16(a), a1 = bf16(a - a0), a2 = bf16(a - a0 - a1)
+// (round to nearest even; every residual is exact in fp32), so
+// |a - a0 - a1 - a2| <= 2^-27 |a|.  The product a . b keeps the six part
+// products of order >= 2^-16 (a0b0, a0b1, a1b0, a0b2, a1b1, a2b0); the three
+// dropped ones are <= 2^-26 |a b| together, below an fp32 product's 2^-24
+// rounding.  Each part product is exact in fp32 (8 x 8 significant bits) and
+// v_mfma_f32_32x32x16_bf16 sums them into an fp32 accumulator, so a 32x32x16
+// block is 6 bf16 MFMAs (6 x 32 cycles) instead of 8 fp32 32x32x2 MFMAs
+// (8 x 64 cycles) at fp32 accuracy (tools/micro/split_bf16.hip measures it).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "mfma.hpp"
+
+namespace srcnn {
+namespace mfma {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void split3(float a, __bf16& p0, __bf16& p1, __bf16& p2) {
+  p0 = (__bf16)a;
+  const float r = a - (float)p0;
+  p1 = (__bf16)r;
+  p2 = (__bf16)(r - (float)p1);
+}
+
+// eight values -> the three part operands of one 32x32x16 fragment
+__device__ __forceinline__ void split8(const float (&v)[8], bf16x8 (&o)[3]) {
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    __bf16 p0, p1, p2;
+    split3(v[j], p0, p1, p2);
+    o[0][j] = p0;
+    o[1][j] = p1;
+    o[2][j] = p2;
+  }
+}
+
+// max(x, 0) as one v_max_i32 on the bit pattern (a negative float is a
+// negative int32; fmaxf adds a canonicalising v_max per value)
+__device__ __forceinline__ float relu1(float x) {
+  const int b = __builtin_bit_cast(int, x);
+  return __builtin_bit_cast(float, b > 0 ? b : 0);
+}
+
+__device__ __forceinline__ f32x16 mma_bf16(const bf16x8& a, const bf16x8& b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// c += a . b over a 16-slot k-step, the six part products, small ones first
+__device__ __forceinline__ f32x16 mma_x6(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x16 c) {
+  c = mma_bf16(a[2], b[0], c);
+  c = mma_bf16(a[1], b[1], c);
+  c = mma_bf16(a[0], b[2], c);
+  c = mma_bf16(a[1], b[0], c);
+  c = mma_bf16(a[0], b[1], c);
+  return mma_bf16(a[0], b[0], c);
+}
+
+}  // namespace mfma
+}  // namespace srcnn

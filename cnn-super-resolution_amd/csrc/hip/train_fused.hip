@@ -31,6 +31,7 @@
 #include "common.hpp"
 #include "mfma.hpp"
 #include "ops.hpp"
+#include "split.hpp"
 
 namespace srcnn {
 namespace fused {
@@ -348,6 +349,7 @@ __global__ __launch_bounds__(256, 2) void l12_fwd_kernel(
   SRCNN_CLOCK_END(g_clk, 0);
 }
 
+#include "l12x6.hpp"
 #include "l3_delta.hpp"
 #include "l3r.hpp"
 
@@ -904,6 +906,22 @@ static int launch_l3r(const float* A2, const float* T, const float* W3, const fl
   return SRCNN_OK;
 }
 
+// 79 KB of LDS for 33x33 tiles: two blocks per CU
+static int launch_l12x6(const float* X, const float* W1, const float* B1, const float* W2, const float* B2,
+                        float* A1, float* A2, const Geom& g, const LazyUpdate* lz, int grid, hipStream_t s) {
+  const void* k = lz ? (const void*)l12x6_fwd_kernel<true> : (const void*)l12x6_fwd_kernel<false>;
+  hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+  if (e != hipSuccess) return fail(SRCNN_ERR_HIP, "hipFuncSetAttribute(l12x6_fwd): %s", hipGetErrorString(e));
+  const size_t lds = X6Lds(g.W, g.H).bytes;
+  if (lz)
+    hipLaunchKernelGGL((l12x6_fwd_kernel<true>), dim3(grid), dim3(256), lds, s, X, W1, B1, W2, B2, A1, A2, g, *lz);
+  else
+    hipLaunchKernelGGL((l12x6_fwd_kernel<false>), dim3(grid), dim3(256), lds, s, X, W1, B1, W2, B2, A1, A2, g,
+                       LazyUpdate{});
+  SRCNN_LAUNCH_TRY();
+  return SRCNN_OK;
+}
+
 template <int N2, int F3>
 static int launch_l3(const float* A2, const float* T, const float* W3, const float* B3, float* D2,
                      float* slab3, float* sqs, float* A3, const L3Geom& lg, int grid, size_t lds,
@@ -944,6 +962,8 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
       l3r || (lds3 <= 160 * 1024 && w3 * h3 <= kL3MaxOut &&
               ((ow * oh + 15) / 16 + kL3Threads / 64 - 1) / (kL3Threads / 64) <= L3Lds<N2, F3>::kUnitsPerWave);
   const int g12 = grid_for_batch(batch, kL12Grid);
+  // layers 1 + 2 in split-bf16 products (l12x6.hpp) for the default net
+  const bool x6 = N1 == 64 && N2 == 32 && F1 == 9 && g_arith == 0 && l12x6_fits(w, h);
   // l3r: up to 2 resident blocks per CU; between 256 and 1024 samples keep
   // two samples per block, so the second sample's A2 loads run under the first
   // one's delta2 phase (512 tiles: l3 0.0306 -> 0.0295 ms; at batch 4096 a
@@ -990,14 +1010,16 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   Geom g{(int)w, (int)h, ow, oh, (int)batch};
   {
     SRCNN_PROFILE("l12_fwd_mfma", s);
-    kernels_note(lazy ? "l12_fwd_lazy" : "l12_fwd");
-    if (lazy)
+    kernels_note(x6 ? (lazy ? "l12x6_fwd_lazy" : "l12x6_fwd") : lazy ? "l12_fwd_lazy" : "l12_fwd");
+    if (x6) {
+      if (int rc = launch_l12x6(X, W1, B1, W2, B2, A1, A2, g, lazy ? lz : nullptr, g12, s)) return rc;
+    } else if (lazy)
       hipLaunchKernelGGL((l12_fwd_kernel<N1, N2, F1, true>), dim3(g12), dim3(256), 0, s, X, W1,
                          B1, W2, B2, A1, A2, g, *lz);
     else
       hipLaunchKernelGGL((l12_fwd_kernel<N1, N2, F1>), dim3(g12), dim3(256), 0, s, X, W1,
                          B1, W2, B2, A1, A2, g, LazyUpdate{});
-    SRCNN_LAUNCH_TRY();
+    if (!x6) SRCNN_LAUNCH_TRY();
   }
   // lazy, layer 3 on the op-level kernels: they accumulate, so their
   // gradient segment starts from zero (after l12 has read the pending one)
@@ -1079,8 +1101,9 @@ static int preload_one(const srcnn_net* net) {
   const void* k[] = {(const void*)l12_fwd_kernel<N1, N2, F1>, (const void*)l12_fwd_kernel<N1, N2, F1, true>,
                      (const void*)l3_delta_kernel<N2, F3>, (const void*)d1_grad12_kernel<N1, N2, F1>,
                      (const void*)slab_reduce_kernel, (const void*)l3r_delta_kernel<F3>,
-                     (const void*)d1c_grad12_kernel<9>};
-  const int rc = resolve_kernels(k, N1 == 64 && N2 == 32 && F1 == 9 ? 7 : 6);
+                     (const void*)d1c_grad12_kernel<9>, (const void*)l12x6_fwd_kernel<false>,
+                     (const void*)l12x6_fwd_kernel<true>};
+  const int rc = resolve_kernels(k, N1 == 64 && N2 == 32 && F1 == 9 ? 9 : 6);
   return rc ? rc : 1;
 }
 

@@ -103,6 +103,8 @@ SIGNATURES = {
     "srcnn_profile_print": (_I, []),
     "srcnn_profile_clock": (_I, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double)]),
     "srcnn_set_path": (_I, [_I]),
+    "srcnn_set_arith": (_I, [_I]),
+    "srcnn_get_arith": (_I, []),
     "srcnn_get_path": (_I, []),
     "srcnn_last_path": (ctypes.c_char_p, []),
     "srcnn_last_kernels": (ctypes.c_char_p, []),
@@ -398,6 +400,15 @@ def forward(net, X, w, h, batch, params, out, ws, ws_bytes, s=None):
 
 def set_path(p):
     _call("srcnn_set_path", p)
+
+
+def set_arith(a):
+    """0: split-bf16 matrix-core products (default), 1: fp32 MFMA only."""
+    _call("srcnn_set_arith", a)
+
+
+def get_arith():
+    return _lib.srcnn_get_arith()
 
 
 def get_path():

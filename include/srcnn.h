@@ -253,6 +253,14 @@ SRCNN_API int srcnn_profile_clock(const char* kernel, double* ghz);
  * 0 = auto (fast specialisations where the shape matches), 1 = generic only. */
 SRCNN_API int srcnn_set_path(int path);
 SRCNN_API int srcnn_get_path(void);
+/* Matrix-core arithmetic of the fused default-net kernels (A/B and parity):
+ * 0 = split bf16 (default): fp32 products as six exact bf16 part products on
+ *     v_mfma_f32_32x32x16_bf16, at fp32 accuracy;
+ * 1 = fp32 MFMA only (v_mfma_f32_32x32x2_f32 / 16x16x4_f32).
+ * SRCNN_ARITH=f32 in the environment starts the library at 1.  The results
+ * of the two differ by fp32 rounding only.  An MI355X extension. */
+SRCNN_API int srcnn_set_arith(int arith);
+SRCNN_API int srcnn_get_arith(void);
 /* Kernel family that served the most recent operator / network call of this
  * thread, so a slow path is never silent:
  *   "fused"   train_fused.hip / forward_fused.hip (nets with f2 == 1)
