@@ -63,7 +63,7 @@ int net_dims(const srcnn_net* net, uint32_t w, uint32_t h, NetDims* d) {
   d->w3 = d->w2 - net->f3 + 1;
   d->h3 = d->h2 - net->f3 + 1;
   d->s1 = (size_t)d->w1 * d->h1 * net->n1;
-  d->s1p = ((size_t)d->w1 * d->h1 + 31) / 32 * 32 * net->n1;
+  d->s1p = srcnn::fused::a1_chunks(d->w1, d->h1) * 32 * net->n1;
   d->s2 = (size_t)d->w2 * d->h2 * net->n2;
   d->s3 = (size_t)d->w3 * d->h3;
   return SRCNN_OK;
@@ -485,8 +485,9 @@ int srcnn_train_activations(const srcnn_net* net, uint32_t w, uint32_t h, uint32
                                                     nullptr, nullptr, nullptr, nullptr, nullptr,
                                                     nullptr, nullptr, nullptr, 0, nullptr, true,
                                                     &unused) == 1;
-  int rc = blocked ? srcnn::fused::unblock_a1(L.A1, A1, net->n1, d.w1 * d.h1, batch, s)
-                   : srcnn_memcpy_d2d(A1, L.A1, d.s1 * batch * sizeof(float), stream);
+  int rc = blocked && srcnn::fused::a1_runs(net, w, h) ? srcnn::fused::unrun_a1(L.A1, A1, d.w1, d.h1, batch, s)
+           : blocked ? srcnn::fused::unblock_a1(L.A1, A1, net->n1, d.w1 * d.h1, batch, s)
+                     : srcnn_memcpy_d2d(A1, L.A1, d.s1 * batch * sizeof(float), stream);
   if (rc) return rc;
   if ((rc = srcnn_memcpy_d2d(A2, L.A2, d.s2 * batch * sizeof(float), stream))) return rc;
   return srcnn_memcpy_d2d(A3, L.A3, d.s3 * batch * sizeof(float), stream);

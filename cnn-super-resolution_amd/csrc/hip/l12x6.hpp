@@ -40,6 +40,8 @@ constexpr int kX6KS = 5;                  // bf16 k-steps of layer 1
 constexpr int kX6W1 = kX6KS * 2 * 3 * 512;  // W1 image, bf16: [s][t][part][lane][8]
 constexpr int kX6W2 = 4 * 3 * 512;          // W2 image, bf16: [m][part][lane][8]
 
+// per wave: the A2 regroup scratch [32 slots][kL12A2S] and the slots' pixels
+constexpr int kX6Sc = 32 * kL12A2S + 32;
 struct X6Lds {
   int r, xs, a2sc, bytes;  // byte offsets of the pair images, the fp32 tile, the A2 scratch
   __host__ __device__ X6Lds(int w, int h) {
@@ -48,7 +50,7 @@ struct X6Lds {
     r = base;
     xs = r + 3 * (n + 1) * 4;
     a2sc = (xs + n * 4 + 15) & ~15;
-    bytes = a2sc + 4 * 32 * kL12A2S * 4;
+    bytes = a2sc + 4 * kX6Sc * 4;
   }
 };
 
@@ -63,7 +65,8 @@ __global__ __launch_bounds__(256, 2) void l12x6_fwd_kernel(const float* __restri
                                                             const float* __restrict__ W2,
                                                             const float* __restrict__ B2,
                                                             float* __restrict__ A1,
-                                                            float* __restrict__ A2, Geom g, LazyUpdate lz) {
+                                                            float* __restrict__ A2, Geom g, RunGeom rg,
+                                                            LazyUpdate lz) {
   constexpr int N1 = 64, N2 = 32, F1 = 9, NT1 = 2;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const X6Lds L(g.W, g.H);
@@ -79,7 +82,7 @@ __global__ __launch_bounds__(256, 2) void l12x6_fwd_kernel(const float* __restri
   const int lane = mfma::lane_id(), wave = mfma::wave_id();
   const int h = lane >> 5, li = lane & 31;
   const int W = g.W, xn = g.W * g.H;
-  const int npx = g.ow * g.oh, nch = (npx + 31) / 32;
+  const int npx = g.ow * g.oh, nch = rg.nch;
   const int rn = xn + 1;  // pair-image dwords per part
 
   float xr[kL12Regs];
@@ -156,29 +159,30 @@ __global__ __launch_bounds__(256, 2) void l12x6_fwd_kernel(const float* __restri
   for (int t = 0; t < NT1; t++) a88r[t] = a88s[64 * h + 32 * t + li];
 
   // ---- software-pipelined stores of the previous chunk (as in l12_fwd) ----
-  constexpr int NST = 4 * NT1 + N2 / 8;
+  // A1 leaves TRANSPOSED per chunk, [chunk][64 channels][32 slots] (d1x6
+  // reads a channel's slots as 16-B runs): store k < 32 is register k & 15
+  // of tile k >> 4, every half-wave writing one channel's 128 B.  A2 leaves
+  // as whole 128-B pixel rows at the slots' pixels (runs.hpp order).
+  constexpr int NST = 32 * NT1 / 2 + N2 / 8;
   f32x16 pa1[NT1], pa2 = zero16();
 #pragma unroll
   for (int t = 0; t < NT1; t++) pa1[t] = zero16();
   bool pok = false;
   float* pa1p = A1;
   float* pa2p = A2;
-  int pc0 = 0;
+  int ppx[4] = {-1, -1, -1, -1};  // pixels of the A2 row stores (-1: dummy slot)
   auto store_prev = [&](int k) {
     if (pok) {
-      if (k < 4 * NT1) {
-        const int t = k / 4, q = k % 4;
-        f32x4 v_;
-#pragma unroll
-        for (int e = 0; e < 4; e++) v_[e] = pa1[t][4 * q + e];
-        __builtin_nontemporal_store(v_, reinterpret_cast<f32x4*>(pa1p + 256 * k));
+      if (k < 16 * NT1) {
+        const int t = k >> 4, r = k & 15;
+        __builtin_nontemporal_store(pa1[t][r], pa1p + (32 * t + crow(r, h)) * 32);
       } else {
-        const int q = k - 4 * NT1;
-        if (pc0 + 8 * q + (lane >> 3) < npx) {
+        const int q = k - 16 * NT1;
+        if (ppx[q] >= 0) {
           f32x4 v_;
 #pragma unroll
           for (int e = 0; e < 4; e++) v_[e] = pa2[4 * q + e];
-          *reinterpret_cast<f32x4*>(pa2p + (8 * q + (lane >> 3)) * N2 + 4 * (lane & 7)) = v_;
+          *reinterpret_cast<f32x4*>(pa2p + (size_t)ppx[q] * N2 + 4 * (lane & 7)) = v_;
         }
       }
     }
@@ -215,9 +219,8 @@ __global__ __launch_bounds__(256, 2) void l12x6_fwd_kernel(const float* __restri
     if (sample + (int)gridDim.x < g.batch) xload(sample + gridDim.x);
 
     for (int c = wave; c < nch; c += 4) {
-      const int pl = c * 32 + li;
-      const int pc = min(pl, npx - 1);
-      const int iy = pc / g.ow, ix = pc - iy * g.ow;
+      int iy, ix;
+      const bool pv = slot_coord(rg, c, li, iy, ix);
       const int rb = (iy + h) * W + ix;  // row 2s + h of k-steps 0-3
       // k-step 4: half 0 row 8 (dx 0..7), half 1 column 8 (dy 0..7)
       const int b4 = h ? iy * W + ix + 8 : (iy + 8) * W + ix, st4 = h ? W : 1;
@@ -263,7 +266,8 @@ __global__ __launch_bounds__(256, 2) void l12x6_fwd_kernel(const float* __restri
         if (gi == 6) split8(x4, xb[0]);
         __builtin_amdgcn_sched_barrier(0);
         acc1[t] = mma_x6(wa[gi & 1], xb[s & 1], acc1[t]);
-        store_prev(gi);
+#pragma unroll
+        for (int k = 3 * gi; k < 3 * gi + 3; k++) store_prev(k);
         __builtin_amdgcn_sched_barrier(0);
       }
 #pragma unroll
@@ -297,13 +301,17 @@ __global__ __launch_bounds__(256, 2) void l12x6_fwd_kernel(const float* __restri
         __builtin_amdgcn_sched_barrier(0);
         acc2 = mma_x6(wb[m & 1], bb[m & 1], acc2);
         if (m + 1 < 4) a1split(m + 1, bb[(m + 1) & 1]);
-        if (m < 2) store_prev(10 + m);
+        if (m < 3) {
+          store_prev(30 + 2 * m);
+          store_prev(31 + 2 * m);
+        }
         __builtin_amdgcn_sched_barrier(0);
       }
 #pragma unroll
       for (int t = 0; t < NT1; t++) pa1[t] = acc1[t];
       {
-        float* sc = a2sc + wave * 32 * kL12A2S;
+        float* sc = a2sc + wave * kX6Sc;
+        int* scp = reinterpret_cast<int*>(sc + 32 * kL12A2S);
 #pragma unroll
         for (int m = 0; m < 4; m++) {
           f32x4 v_;
@@ -311,18 +319,19 @@ __global__ __launch_bounds__(256, 2) void l12x6_fwd_kernel(const float* __restri
           for (int e = 0; e < 4; e++) v_[e] = relu1(acc2[4 * m + e]);
           *reinterpret_cast<f32x4*>(sc + li * kL12A2S + 8 * m + 4 * h) = v_;
         }
+        if (h == 0) scp[li] = pv ? iy * g.ow + ix : -1;
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
         for (int q = 0; q < 4; q++) {
           const f32x4 v_ = *reinterpret_cast<const f32x4*>(sc + (8 * q + (lane >> 3)) * kL12A2S + 4 * (lane & 7));
 #pragma unroll
           for (int e = 0; e < 4; e++) pa2[4 * q + e] = v_[e];
+          ppx[q] = scp[8 * q + (lane >> 3)];
         }
-        pc0 = c * 32;
       }
       pok = true;
-      pa1p = A1 + ((size_t)sample * nch + c) * (32 * N1) + 4 * lane;
-      pa2p = A2 + ((size_t)sample * npx + c * 32) * N2;
+      pa1p = A1 + ((size_t)sample * nch + c) * (32 * N1) + li;
+      pa2p = A2 + (size_t)sample * npx * N2;
     }
   }
   // (a sample's last chunk is stored under the next sample's first one)

@@ -140,6 +140,12 @@ __device__ __forceinline__ void lazy_write_slice(const LazyUpdate& u) {
 }
 // held-clock probes (common.hpp): slot 0 l12_fwd, 1 l3_delta, 2 d1_grad12
 int train_clock(int slot, double* ghz);
+// the split-bf16 step (l12x6) stores A1 in run order, transposed per chunk:
+// a1_runs tells whether the fused step takes that path for this net / tile,
+// a1_chunks the A1 chunks per sample either path needs, unrun_a1 converts
+bool a1_runs(const srcnn_net* net, uint32_t w, uint32_t h);
+size_t a1_chunks(uint32_t ow, uint32_t oh);
+int unrun_a1(const float* A1t, float* A1, uint32_t ow, uint32_t oh, uint32_t batch, hipStream_t s);
 // the fused step's blocked A1 (l12_fwd_kernel) -> reference HWC [batch][npx][n1]
 int unblock_a1(const float* A1b, float* A1, uint32_t n1, uint32_t npx, uint32_t batch, hipStream_t s);
 // srcnn_preload: resolve the family's kernels for this net (1 = this family's

@@ -349,7 +349,9 @@ __global__ __launch_bounds__(256, 2) void l12_fwd_kernel(
   SRCNN_CLOCK_END(g_clk, 0);
 }
 
+#include "runs.hpp"
 #include "l12x6.hpp"
+#include "d1x6.hpp"
 #include "l3_delta.hpp"
 #include "l3r.hpp"
 
@@ -906,18 +908,36 @@ static int launch_l3r(const float* A2, const float* T, const float* W3, const fl
   return SRCNN_OK;
 }
 
-// 79 KB of LDS for 33x33 tiles: two blocks per CU
+// the split-bf16 pair (l12x6 + d1x6) serves the default net where both fit
+static bool x6_active(int n1, int n2, int f1, uint32_t w, uint32_t h) {
+  return n1 == 64 && n2 == 32 && f1 == 9 && g_arith == 0 && l12x6_fits(w, h) && d1x6_fits(w, h);
+}
+
+// 78 KB of LDS for 33x33 tiles: two blocks per CU
 static int launch_l12x6(const float* X, const float* W1, const float* B1, const float* W2, const float* B2,
-                        float* A1, float* A2, const Geom& g, const LazyUpdate* lz, int grid, hipStream_t s) {
+                        float* A1, float* A2, const Geom& g, const RunGeom& rg, const LazyUpdate* lz, int grid,
+                        hipStream_t s) {
   const void* k = lz ? (const void*)l12x6_fwd_kernel<true> : (const void*)l12x6_fwd_kernel<false>;
   hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
   if (e != hipSuccess) return fail(SRCNN_ERR_HIP, "hipFuncSetAttribute(l12x6_fwd): %s", hipGetErrorString(e));
   const size_t lds = X6Lds(g.W, g.H).bytes;
   if (lz)
-    hipLaunchKernelGGL((l12x6_fwd_kernel<true>), dim3(grid), dim3(256), lds, s, X, W1, B1, W2, B2, A1, A2, g, *lz);
+    hipLaunchKernelGGL((l12x6_fwd_kernel<true>), dim3(grid), dim3(256), lds, s, X, W1, B1, W2, B2, A1, A2, g, rg,
+                       *lz);
   else
-    hipLaunchKernelGGL((l12x6_fwd_kernel<false>), dim3(grid), dim3(256), lds, s, X, W1, B1, W2, B2, A1, A2, g,
+    hipLaunchKernelGGL((l12x6_fwd_kernel<false>), dim3(grid), dim3(256), lds, s, X, W1, B1, W2, B2, A1, A2, g, rg,
                        LazyUpdate{});
+  SRCNN_LAUNCH_TRY();
+  return SRCNN_OK;
+}
+
+static int launch_d1x6(const float* X, const float* A1, const float* D2, const float* W2, float* slab,
+                       const Geom& g, const RunGeom& rg, int grid, hipStream_t s) {
+  hipError_t e = hipFuncSetAttribute((const void*)d1x6_grad12_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     150 * 1024);
+  if (e != hipSuccess) return fail(SRCNN_ERR_HIP, "hipFuncSetAttribute(d1x6_grad12): %s", hipGetErrorString(e));
+  const size_t lds = D6Lds(g.W, g.H, rg).bytes;
+  hipLaunchKernelGGL(d1x6_grad12_kernel, dim3(grid), dim3(256), lds, s, X, A1, D2, W2, slab, g, rg);
   SRCNN_LAUNCH_TRY();
   return SRCNN_OK;
 }
@@ -962,8 +982,9 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
       l3r || (lds3 <= 160 * 1024 && w3 * h3 <= kL3MaxOut &&
               ((ow * oh + 15) / 16 + kL3Threads / 64 - 1) / (kL3Threads / 64) <= L3Lds<N2, F3>::kUnitsPerWave);
   const int g12 = grid_for_batch(batch, kL12Grid);
-  // layers 1 + 2 in split-bf16 products (l12x6.hpp) for the default net
-  const bool x6 = N1 == 64 && N2 == 32 && F1 == 9 && g_arith == 0 && l12x6_fits(w, h);
+  // split-bf16 products (l12x6.hpp, d1x6.hpp) for the default net
+  const bool x6 = x6_active(N1, N2, F1, w, h);
+  const RunGeom rg = run_geom(ow, oh);
   // l3r: up to 2 resident blocks per CU; between 256 and 1024 samples keep
   // two samples per block, so the second sample's A2 loads run under the first
   // one's delta2 phase (512 tiles: l3 0.0306 -> 0.0295 ms; at batch 4096 a
@@ -978,7 +999,9 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   int d1c_parts = kD1c ? std::max(1, std::min({4, nch1, kD1cGrid / (int)std::max<uint32_t>(batch, 1)})) : 1;
   while (d1c_parts > 1 && (d1c_parts - 1) * ((nch1 + d1c_parts - 1) / d1c_parts) >= nch1)
     d1c_parts--;  // every part holds at least one chunk (the kernel's DMA pipeline assumes it)
-  const int gd = kD1c ? (int)std::min<size_t>((size_t)batch * d1c_parts, kD1cGrid) : grid_for_batch(batch, 512);
+  const int gd6 = grid_for_batch(batch, 256);  // d1x6: 4 slabs (waves) per block
+  const int gd = x6 ? 4 * gd6
+                    : kD1c ? (int)std::min<size_t>((size_t)batch * d1c_parts, kD1cGrid) : grid_for_batch(batch, 512);
   const size_t s12 = (size_t)gd * NetT::P12;
   size_t s3 = (size_t)g3 * NetT::P3, ssq = g3;  // gW3 slabs, squared-error slabs
   if (!l3_fused) {  // the op-level gW3 slabs; the same space serves the squared-error reduction
@@ -1012,7 +1035,7 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
     SRCNN_PROFILE("l12_fwd_mfma", s);
     kernels_note(x6 ? (lazy ? "l12x6_fwd_lazy" : "l12x6_fwd") : lazy ? "l12_fwd_lazy" : "l12_fwd");
     if (x6) {
-      if (int rc = launch_l12x6(X, W1, B1, W2, B2, A1, A2, g, lazy ? lz : nullptr, g12, s)) return rc;
+      if (int rc = launch_l12x6(X, W1, B1, W2, B2, A1, A2, g, rg, lazy ? lz : nullptr, g12, s)) return rc;
     } else if (lazy)
       hipLaunchKernelGGL((l12_fwd_kernel<N1, N2, F1, true>), dim3(g12), dim3(256), 0, s, X, W1,
                          B1, W2, B2, A1, A2, g, *lz);
@@ -1050,14 +1073,16 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   }
   {
     SRCNN_PROFILE("delta1_grad12_fused", s);
-    kernels_note(kD1c ? "d1c_grad12" : "d1_grad12");
-    if (kD1c)
+    kernels_note(x6 ? "d1x6_grad12" : kD1c ? "d1c_grad12" : "d1_grad12");
+    if (x6) {
+      if (int rc = launch_d1x6(X, A1, D2, W2, slab12, g, rg, gd6, s)) return rc;
+    } else if (kD1c)
       hipLaunchKernelGGL((d1c_grad12_kernel<(F1 == 9 ? F1 : 9)>), dim3(gd), dim3(256 * kD1cTeams), d1c_lds_bytes(w, h),
                          s, X, A1, D2, W2, slab12, g, d1c_xs_floats(h), d1c_parts);
     else
       hipLaunchKernelGGL((d1_grad12_kernel<N1, N2, F1>), dim3(gd), dim3(256), 0, s, X, A1, D2, W2,
                          slab12, g);
-    SRCNN_LAUNCH_TRY();
+    if (!x6) SRCNN_LAUNCH_TRY();
   }
   {
     SRCNN_PROFILE("slab_reduce", s);
@@ -1102,8 +1127,8 @@ static int preload_one(const srcnn_net* net) {
                      (const void*)l3_delta_kernel<N2, F3>, (const void*)d1_grad12_kernel<N1, N2, F1>,
                      (const void*)slab_reduce_kernel, (const void*)l3r_delta_kernel<F3>,
                      (const void*)d1c_grad12_kernel<9>, (const void*)l12x6_fwd_kernel<false>,
-                     (const void*)l12x6_fwd_kernel<true>};
-  const int rc = resolve_kernels(k, N1 == 64 && N2 == 32 && F1 == 9 ? 9 : 6);
+                     (const void*)l12x6_fwd_kernel<true>, (const void*)d1x6_grad12_kernel};
+  const int rc = resolve_kernels(k, N1 == 64 && N2 == 32 && F1 == 9 ? 10 : 6);
   return rc ? rc : 1;
 }
 
@@ -1131,6 +1156,46 @@ __global__ void unblock_a1_kernel(const float* __restrict__ A1b, float* __restri
     const int q = r >> 3, hh = (r >> 2) & 1, e = r & 3;
     A1[i] = A1b[(s * nch + c) * (size_t)(32 * n1) + 256 * (4 * t + q) + 4 * (li + 32 * hh) + e];
   }
+}
+
+// l12x6's A1 (runs.hpp order, [chunk][64 channels][32 slots]) -> HWC
+__global__ void unrun_a1_kernel(const float* __restrict__ A1t, float* __restrict__ A1, RunGeom rg,
+                                size_t total) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const int ch = (int)(i % 64);
+    const size_t sp = i / 64;
+    const int p = (int)(sp % ((size_t)rg.ow * rg.oh));
+    const size_t s = sp / ((size_t)rg.ow * rg.oh);
+    const int iy = p / rg.ow, ix = p - iy * rg.ow;
+    int k, e;
+    if (ix < 4 * rg.a) {
+      k = iy * rg.a + ix / 4;
+      e = ix % 4;
+    } else {
+      k = rg.nrow + (ix - 4 * rg.a) * rg.cr + iy / 4;
+      e = iy % 4;
+    }
+    const int c = k / 8, slot = (k % 8) * 4 + e;
+    A1[i] = A1t[((s * rg.nch + c) * 64 + ch) * 32 + slot];
+  }
+}
+
+bool a1_runs(const srcnn_net* net, uint32_t w, uint32_t h) {
+  return net->f2 == 1 && x6_active((int)net->n1, (int)net->n2, (int)net->f1, w, h);
+}
+
+size_t a1_chunks(uint32_t ow, uint32_t oh) {
+  return std::max<size_t>((ow * oh + 31) / 32, run_geom((int)ow, (int)oh).nch);
+}
+
+int unrun_a1(const float* A1t, float* A1, uint32_t ow, uint32_t oh, uint32_t batch, hipStream_t s) {
+  const size_t total = (size_t)batch * ow * oh * 64;
+  if (total == 0) return SRCNN_OK;
+  const int blocks = (int)std::min<size_t>((total + 255) / 256, 4096);
+  hipLaunchKernelGGL(unrun_a1_kernel, dim3(blocks), dim3(256), 0, s, A1t, A1, run_geom((int)ow, (int)oh), total);
+  SRCNN_LAUNCH_TRY();
+  return SRCNN_OK;
 }
 
 int unblock_a1(const float* A1b, float* A1, uint32_t n1, uint32_t npx, uint32_t batch, hipStream_t s) {
