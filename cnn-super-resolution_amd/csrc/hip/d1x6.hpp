@@ -242,7 +242,7 @@ __global__ __launch_bounds__(256, 1) void d1x6_grad12_kernel(const float* __rest
         float v[8];
 #pragma unroll
         for (int j = 0; j < 8; j++) v[j] = d2c[2 * k + (j >> 2)][j & 3];
-        split8(v, da[k]);
+        split8_pk(v, da[k]);
       }
       f32x16 d1[2];
 #pragma unroll
@@ -265,7 +265,7 @@ __global__ __launch_bounds__(256, 1) void d1x6_grad12_kernel(const float* __rest
         float v[8];
 #pragma unroll
         for (int j = 0; j < 8; j++) v[j] = d2t[8 * m + j];
-        split8(v, db[m]);
+        split8_pk(v, db[m]);
       }
 #pragma unroll
       for (int r = 0; r < 16; r++) gb2 += d2t[r];
@@ -277,7 +277,7 @@ __global__ __launch_bounds__(256, 1) void d1x6_grad12_kernel(const float* __rest
 #pragma unroll
           for (int j = 0; j < 8; j++) v[j] = a1c[t][2 * m + (j >> 2)][j & 3];
           bf16x8 a[3];
-          split8(v, a);
+          split8_pk(v, a);
           g2[t] = mma_x6(a, db[m], g2[t]);
         }
 
@@ -302,7 +302,7 @@ __global__ __launch_bounds__(256, 1) void d1x6_grad12_kernel(const float* __rest
           float v[8];
 #pragma unroll
           for (int j = 0; j < 8; j++) v[j] = d1[t][8 * m + j];
-          split8(v, a1x[t]);
+          split8_pk(v, a1x[t]);
         }
 #pragma unroll
         for (int u = 0; u < 3; u++) {

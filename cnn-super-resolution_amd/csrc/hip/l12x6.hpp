@@ -34,6 +34,7 @@ using mfma::mma_x6;
 using mfma::relu1;
 using mfma::split3;
 using mfma::split8;
+using mfma::split8_pk;
 using mfma::u32x4;
 
 constexpr int kX6KS = 5;                  // bf16 k-steps of layer 1

@@ -30,15 +30,46 @@ __device__ __forceinline__ void split3(float a, __bf16& p0, __bf16& p1, __bf16& 
   p2 = (__bf16)(r - (float)p1);
 }
 
-// eight values -> the three part operands of one 32x32x16 fragment
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+// split8 with the residual subtractions as packed v_pk_add_f32 (d1x6, one
+// wave per SIMD: the fewer VALU instructions won there, same-box A/B)
+__device__ __forceinline__ void split8_pk(const float (&v)[8], bf16x8 (&o)[3]) {
+#pragma unroll
+  for (int j = 0; j < 8; j += 2) {
+    const f32x2 a = {v[j], v[j + 1]};
+    const bf16x2 p0 = __builtin_convertvector(a, bf16x2);
+    const f32x2 r = a - __builtin_convertvector(p0, f32x2);
+    const bf16x2 p1 = __builtin_convertvector(r, bf16x2);
+    const bf16x2 p2 = __builtin_convertvector(r - __builtin_convertvector(p1, f32x2), bf16x2);
+    o[0][j] = p0[0];
+    o[0][j + 1] = p0[1];
+    o[1][j] = p1[0];
+    o[1][j + 1] = p1[1];
+    o[2][j] = p2[0];
+    o[2][j + 1] = p2[1];
+  }
+}
+
+// eight values -> the three part operands of one 32x32x16 fragment, two
+// values per conversion (one v_cvt_pk_bf16_f32 per pair and part)
 __device__ __forceinline__ void split8(const float (&v)[8], bf16x8 (&o)[3]) {
 #pragma unroll
-  for (int j = 0; j < 8; j++) {
-    __bf16 p0, p1, p2;
-    split3(v[j], p0, p1, p2);
-    o[0][j] = p0;
-    o[1][j] = p1;
-    o[2][j] = p2;
+  for (int j = 0; j < 8; j += 2) {
+    const bf16x2 p0 = __builtin_convertvector((f32x2){v[j], v[j + 1]}, bf16x2);
+    const f32x2 h0 = __builtin_convertvector(p0, f32x2);
+    // (scalar subtractions: v_pk_add_f32 beside MFMAs costs more issue time)
+    const float r0 = v[j] - h0[0], r1 = v[j + 1] - h0[1];
+    const bf16x2 p1 = __builtin_convertvector((f32x2){r0, r1}, bf16x2);
+    const f32x2 h1 = __builtin_convertvector(p1, f32x2);
+    const bf16x2 p2 = __builtin_convertvector((f32x2){r0 - h1[0], r1 - h1[1]}, bf16x2);
+    o[0][j] = p0[0];
+    o[0][j + 1] = p0[1];
+    o[1][j] = p1[0];
+    o[1][j + 1] = p1[1];
+    o[2][j] = p2[0];
+    o[2][j + 1] = p2[1];
   }
 }
 

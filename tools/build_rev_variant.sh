@@ -7,13 +7,15 @@ R=$(cd "$(dirname "$0")/.." && pwd)
 name=$1; rev=$2
 T=/tmp/srcnn_rev_$name
 rm -rf $T && mkdir -p $T
-(cd $R && git archive "$rev" include cnn-super-resolution_amd/csrc) | tar -x -C $T
+(cd $R && git archive "$rev" include cnn-super-resolution_amd/csrc cnn-super-resolution_amd/Makefile) | tar -x -C $T
 P=$R/cnn-super-resolution_amd
 O=$T/obj
 mkdir -p $O $P/lib/variants
 for f in $(cd $T/cnn-super-resolution_amd/csrc/hip && ls *.cpp *.hip); do
+  # that revision's per-file flags (FILEFLAGS_<file> := ... in its Makefile)
+  ff=$(sed -n "s/^FILEFLAGS_$f := //p" $T/cnn-super-resolution_amd/Makefile)
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -fvisibility=hidden -munsafe-fp-atomics \
-    -Wno-unused-result -I$T/include -I$T/cnn-super-resolution_amd/csrc/hip -x hip \
+    -Wno-unused-result -I$T/include -I$T/cnn-super-resolution_amd/csrc/hip $ff -x hip \
     -c $T/cnn-super-resolution_amd/csrc/hip/$f -o $O/$f.o &
 done
 wait

@@ -8,8 +8,10 @@ name=$1; shift
 O=$P/build/variant_$name
 mkdir -p $O $P/lib/variants
 for f in $(cd $P/csrc/hip && ls *.cpp *.hip); do
+  # the Makefile's per-file flags (FILEFLAGS_<file> := ...)
+  ff=$(sed -n "s/^FILEFLAGS_$f := //p" $P/Makefile)
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -fvisibility=hidden -munsafe-fp-atomics \
-    -Wno-unused-result -I$R/include -I$P/csrc/hip "$@" -x hip -c $P/csrc/hip/$f -o $O/$f.o &
+    -Wno-unused-result -I$R/include -I$P/csrc/hip $ff "$@" -x hip -c $P/csrc/hip/$f -o $O/$f.o &
 done
 wait
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $P/lib/variants/libsrcnn_hip_$name.so $O/*.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
