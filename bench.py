@@ -43,6 +43,24 @@ PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA peak
 PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 NOMINAL_CLOCK_GHZ = 2.4    # MI355X_MICROARCH.md: max clock, the clock PEAK_FP32_TFLOPS assumes
 RIDGE = PEAK_FP32_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9)
+# split-bf16 kernels (srcnn_set_arith 0: l12x6, d1x6) form each fp32 product
+# from six bf16 part products on v_mfma_f32_32x32x16_bf16: their matrix-core
+# ceiling in fp32-equivalent FLOP/s is the dense BF16 peak (MI355X_MICROARCH.md:
+# 1024 FLOP/cycle/SIMD x 1024 SIMDs x 2.4 GHz) / 6
+PEAK_BF16_TFLOPS = 2516.6
+PEAK_SPLIT_TFLOPS = round(PEAK_BF16_TFLOPS / 6, 1)
+SPLIT_KERNELS = {"l12x6_fwd": "l12_fwd_mfma", "l12x6_fwd_lazy": "l12_fwd_mfma", "d1x6_grad12": "delta1_grad12_fused"}
+
+
+def split_profiled(S):
+    """Profiler names of the kernels of the last step that ran split-bf16."""
+    try:
+        ks = S.last_kernels()
+    except Exception:
+        return set()
+    if isinstance(ks, str):
+        ks = ks.split(",")
+    return {SPLIT_KERNELS[k] for k in ks if k in SPLIT_KERNELS}
 
 DEFAULT_NET = (64, 32, 9, 1, 5)
 TILE = 33
@@ -179,7 +197,7 @@ def add_clock(out, ghz):
 
 
 def roofline_of(name, launches_per_step, ms_per_step, work, tiles, pmc=None, net=DEFAULT_NET,
-                w=TILE, h=TILE):
+                w=TILE, h=TILE, split=False):
     kw = kernel_work(name, work, net, w, h)
     if not kw or ms_per_step <= 0:
         return None
@@ -199,6 +217,12 @@ def roofline_of(name, launches_per_step, ms_per_step, work, tiles, pmc=None, net
                "frac": round(ach / PEAK_HBM_GBS, 4)}
     out.update({"traffic": traffic, "kernel": name, "avg_launch_ms": round(dur_s * 1e3, 5),
                 "algorithmic_flops_per_launch": int(flops), "algorithmic_bytes_per_launch": int(nbytes)})
+    if split and out["bound"] == "mfma":
+        # "peak" stays the FP32 dense peak (the dtype's); the split kernels'
+        # own matrix-core ceiling beside it
+        out["arith"] = "split-bf16 x6"
+        out["split_peak"] = PEAK_SPLIT_TFLOPS
+        out["frac_of_split_peak"] = round(out["achieved"] / PEAK_SPLIT_TFLOPS, 4)
     return out
 
 
@@ -920,6 +944,7 @@ def run(args, S, parallel, rank, world, local, device=None):
                                                graph_mode, backend, dev, sync)
     _mark("headline timed steps done")
     kernel_path = S.last_path()
+    split = split_profiled(S)  # (the step's own kernels: read before the side legs run)
     stats = S.profile_stats()
     finish(step)
 
@@ -962,7 +987,7 @@ def run(args, S, parallel, rank, world, local, device=None):
             kernels[name] = {"launches_per_step": cnt / n_prof, "ms_per_step": round(ms / n_prof, 4)}
         rooflines = {}
         for name, (cnt, ms) in stats.items():
-            r = roofline_of(name, cnt / n_prof, ms / n_prof, work, B, pmc)
+            r = roofline_of(name, cnt / n_prof, ms / n_prof, work, B, pmc, split=name in split)
             if r:
                 rooflines[name] = add_clock(r, held_clock(S, name))
         dominant = max(rooflines, key=lambda k: stats[k][1]) if rooflines else None
@@ -1010,6 +1035,9 @@ def run(args, S, parallel, rank, world, local, device=None):
             "config": {"workload": workload, "global_batch": global_tiles, "batch_per_gpu": B,
                        "tile": "33x33", "parallelism": "dp%d" % world,
                        "kernel_path": kernel_path,
+                       "mfma_arith": ("split-bf16 x6: fp32 operands as three exact bf16 parts, six part "
+                                      "products per k-step on v_mfma_f32_32x32x16_bf16 (fp32 accuracy, "
+                                      "tests/test_split_arith_gpu.py)" if split else "fp32 MFMA"),
                        "hip_graph": used_graph,
                        "settle_steps": n_settle,
                        "step_call": step_call,

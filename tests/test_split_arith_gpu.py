@@ -1,0 +1,78 @@
+"""Split-bf16 arithmetic (srcnn_set_arith 0, l12x6 / d1x6) against the fp32
+MFMA kernels (srcnn_set_arith 1), both against the double-precision oracle.
+
+The fused default-net step forms its layer-1/2 products from three exact
+bf16 parts per fp32 operand and six part products (csrc/hip/split.hpp).  The
+claim is fp32 accuracy: on the same inputs its normwise error against the
+fp64 computation must stay within the fp32 kernels' own (x 1.5, plus a
+2^-24 floor), gradient segment by segment, and the parameters after an SGD
+step likewise.  The fp32 oracle's error is printed beside them."""
+import numpy as np
+import pytest
+
+import srcnn_oracle as orc
+from hip_util import log_record, make_batch, make_params
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+NET = (64, 32, 9, 1, 5)
+NAMES = ["W1", "B1", "W2", "B2", "W3", "B3"]
+
+
+@pytest.fixture(scope="module")
+def S():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import srcnn_amd
+    yield srcnn_amd
+    srcnn_amd.set_arith(0)
+
+
+def D(a):
+    return torch.from_numpy(np.ascontiguousarray(a, np.float32)).cuda()
+
+
+def H(t):
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+def normwise(got, ref64):
+    got = np.asarray(got, np.float64)
+    ref64 = np.asarray(ref64, np.float64)
+    return float(np.linalg.norm(got - ref64) / max(np.linalg.norm(ref64), 1e-300))
+
+
+def grads(S, arith, X, T, size, batch, params, g0):
+    S.set_arith(arith)
+    net = S.Net(*NET)
+    nbytes = S.train_workspace_bytes(net, size, size, batch)
+    ws = torch.empty(nbytes // 4 + 64, dtype=torch.float32, device="cuda")
+    g = D(g0)
+    err = torch.zeros(1, dtype=torch.float32, device="cuda")
+    S.train_fwd_bwd(net, D(X), D(T), size, size, batch, D(params), g, err, ws, nbytes)
+    return H(g), S.last_kernels()
+
+
+@pytest.mark.parametrize("batch,size,sd", [(64, 33, 0.05), (600, 33, 0.05), (256, 33, 1e-3), (7, 25, 0.05)])
+def test_split_arith_within_fp32_error(S, batch, size, sd):
+    rng = np.random.default_rng(7)
+    X, T = make_batch(rng, batch, size, size)
+    params = make_params(rng, NET, sd=sd)
+    P = params.size
+    g0 = np.zeros(P, np.float32)
+    g32, _ = orc.train_fwd_bwd(NET, X, T, size, size, batch, params, g0)
+    g64, _ = orc.f64.train_fwd_bwd(NET, X, T, size, size, batch, params, g0)
+    gs, ks = grads(S, 0, X, T, size, batch, params, g0)
+    gf, kf = grads(S, 1, X, T, size, batch, params, g0)
+    assert "l12x6_fwd" in ks and "d1x6_grad12" in ks, ks
+    assert "l12_fwd" in kf and "x6" not in kf, kf
+    off = S.net_offsets(S.Net(*NET)) + [P]
+    for i, nm in enumerate(NAMES):
+        sl = slice(off[i], off[i + 1])
+        es, ef, eo = normwise(gs[sl], g64[sl]), normwise(gf[sl], g64[sl]), normwise(g32[sl], g64[sl])
+        log_record({"test": "split_arith", "batch": batch, "size": size, "sd": sd, "seg": nm,
+                    "err_split": es, "err_f32_mfma": ef, "err_f32_oracle": eo})
+        print("%s batch %d: split %.3e  fp32 MFMA %.3e  fp32 oracle %.3e" % (nm, batch, es, ef, eo))
+        assert es <= 1.5 * ef + 2.0 ** -24, (nm, es, ef)
