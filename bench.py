@@ -400,6 +400,9 @@ def forward_4k(S, net_t, frames=20, warmup=3, w=3840, h=2160, settle_ms=50.0):
         kroof = {"bound": "mfma", "achieved": round(ach, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                  "frac": round(ach / PEAK_FP32_TFLOPS, 4), "kernel": kname, "avg_launch_ms": round(kdur * 1e3, 5),
                  "algorithmic_flops_per_launch": int(flops), "traffic": None}
+        if tuple(net_t) == DEFAULT_NET and S.get_arith() == 0:  # fwd_l123x6 (split-bf16)
+            kroof.update({"arith": "split-bf16 x6", "split_peak": PEAK_SPLIT_TFLOPS,
+                          "frac_of_split_peak": round(ach / PEAK_SPLIT_TFLOPS, 4)})
     res = {"frame": "%dx%d" % (w, h), "frames": frames, "settle_frames": n_settle, "ms_per_frame": round(ms, 4),
            "mpix_s": round(w * h / (ms * 1e-3) / 1e6, 1),
            "tflops": round(flops / (ms * 1e-3) / 1e12, 2),

@@ -23,6 +23,7 @@
 #include "common.hpp"
 #include "mfma.hpp"
 #include "ops.hpp"
+#include "split.hpp"
 
 namespace srcnn {
 namespace fused {
@@ -289,6 +290,305 @@ __global__ __launch_bounds__(256, 2) void fwd_l123_kernel(
   SRCNN_CLOCK_END(g_clk_fwd, 0);
 }
 
+
+// ---------------------------------------------------------------------------
+// fwd_l123x6: fwd_l123 for the reference default net (64/32/9/5) with its
+// three GEMMs in split-bf16 products (split.hpp; l12x6.hpp in
+// train_fused.hip has the same L1 / L2 operand scheme):
+//   L1^T  80 taps in 5 bf16 k-steps (slot 8h + j of k-step s: tap (2s+h, j)
+//         for 2s+h <= 8, tap (j, 8) for the last half-step), B operand from
+//         part-interleaved pair images of the region's input tile (rows
+//         2s + h: two ds_read2_b32 per part), tap (8, 8) and B1 in one fp32
+//         32x32x2 MFMA that starts the accumulator
+//   L2^T  the ReLU'd L1 accumulator split in registers against W2 images
+//   Q^T   the ReLU'd L2 accumulator split against W3 images (2 k-steps)
+// Eight waves share one block (and the 48 KB of split weight images) per
+// CU, two per SIMD; a region is 24 rows (3 chunks per wave).
+constexpr int kF6Waves = 8;
+constexpr int kF6Rh = 24;              // region rows
+constexpr int kF6TW = kFwdRW + 8;      // input tile row stride (f1 = 9)
+constexpr int kF6XR = kF6Rh + 8;       // input tile rows
+constexpr int kF6QS = 41;              // Q^T row stride (32 + 2 (f3 - 1) columns)
+constexpr int kF6W1 = 5 * 2 * 3 * 512; // bf16: [s][t][part][lane][8]
+constexpr int kF6W2 = 4 * 3 * 512;     // bf16: [m][part][lane][8]
+constexpr int kF6W3 = 2 * 3 * 512;     // bf16: [m][part][lane][8]
+struct F6Lds {
+  static constexpr int w1 = 0, w2 = w1 + kF6W1 * 2, w3 = w2 + kF6W2 * 2, a88 = w3 + kF6W3 * 2,
+                       b2 = a88 + 128 * 4, r = b2 + 32 * 4,
+                       rn = kF6TW * kF6XR + 1,  // pair-image dwords per part
+                       xs = r + 3 * rn * 4, qs = (xs + kF6TW * kF6XR * 4 + 15) & ~15,
+                       accs = qs + kF6Waves * 25 * kF6QS * 4, bytes = accs + 5 * (kF6Rh + 4) * (kFwdRW + 4) * 4;
+};
+
+__global__ __launch_bounds__(512, 1) void fwd_l123x6_kernel(
+    const float* __restrict__ X, const float* __restrict__ W1, const float* __restrict__ B1,
+    const float* __restrict__ W2, const float* __restrict__ B2, const float* __restrict__ W3,
+    float* __restrict__ part, FwdGeom g) {
+  using mfma::bf16x8;
+  using mfma::mma_x6;
+  using mfma::relu1;
+  using mfma::split3;
+  using mfma::split8;
+  using mfma::u32x4;
+  constexpr int N1 = 64, N2 = 32, F1 = 9, F3 = 5, K3 = F3 * F3, NT1 = 2;
+  constexpr int TW = kF6TW, EW = kFwdRW + F3 - 1, EHM = kF6Rh + F3 - 1;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  char* const base = reinterpret_cast<char*>(smem);
+  __bf16* const w1i = reinterpret_cast<__bf16*>(base + F6Lds::w1);
+  __bf16* const w2i = reinterpret_cast<__bf16*>(base + F6Lds::w2);
+  __bf16* const w3i = reinterpret_cast<__bf16*>(base + F6Lds::w3);
+  float* const a88s = reinterpret_cast<float*>(base + F6Lds::a88);
+  float* const b2i = reinterpret_cast<float*>(base + F6Lds::b2);
+  uint32_t* const rimg = reinterpret_cast<uint32_t*>(base + F6Lds::r);
+  float* const xs = reinterpret_cast<float*>(base + F6Lds::xs);
+  float* const qs = reinterpret_cast<float*>(base + F6Lds::qs);
+  float* const accs = reinterpret_cast<float*>(base + F6Lds::accs);
+  constexpr int rn = F6Lds::rn;
+
+  SRCNN_CLOCK_BEGIN();
+  const int lane = mfma::lane_id(), wave = mfma::wave_id();
+  const int h = lane >> 5, li = lane & 31;
+  const int EH = g.rh + F3 - 1;
+  const int per_frame = g.nrx * g.nry;
+  const int n_items = g.batch * per_frame;
+  constexpr int kXR = (TW * kF6XR + 511) / 512;
+  float xr[kXR];
+  auto xload = [&](int wi) {
+    const int n = wi / per_frame, rr = wi - n * per_frame;
+    const int ry = rr / g.nrx, rx = rr - ry * g.nrx;
+    const int oy0 = ry * g.rh, ox0 = rx * kFwdRW;
+    const int th = min(g.rh, g.oh - oy0) + F1 - 1, tw = min(kFwdRW, g.ow - ox0) + F1 - 1;
+    const float* xsrc = X + (size_t)n * g.W * g.H + (size_t)oy0 * g.W + ox0;
+#pragma unroll
+    for (int k = 0; k < kXR; k++) {
+      const int i = threadIdx.x + 512 * k;
+      const int iy = i / TW, ix = i - iy * TW;
+      xr[k] = (i < th * TW && ix < tw) ? xsrc[(size_t)iy * g.W + ix] : 0.0f;
+    }
+  };
+  if ((int)blockIdx.x < n_items) xload(blockIdx.x);
+
+  // ---- split weight images ----
+  for (int e = threadIdx.x; e < 5 * 2 * 64 * 8; e += 512) {
+    const int j = e & 7, L_ = (e >> 3) & 63, t = (e >> 9) & 1, s_ = e >> 10;
+    const int gg = 2 * s_ + (L_ >> 5);
+    const int tap = gg <= 8 ? gg * F1 + j : j * F1 + 8;
+    __bf16 p[3];
+    split3(W1[tap * N1 + 32 * t + (L_ & 31)], p[0], p[1], p[2]);
+#pragma unroll
+    for (int q = 0; q < 3; q++) w1i[((s_ * 2 + t) * 3 + q) * 512 + L_ * 8 + j] = p[q];
+  }
+  for (int e = threadIdx.x; e < 4 * 64 * 8; e += 512) {
+    const int j = e & 7, L_ = (e >> 3) & 63, m = e >> 9;
+    const int c = 32 * (m >> 1) + crow(8 * (m & 1) + j, L_ >> 5);
+    __bf16 p[3];
+    split3(W2[c * N2 + (L_ & 31)], p[0], p[1], p[2]);
+#pragma unroll
+    for (int q = 0; q < 3; q++) w2i[(m * 3 + q) * 512 + L_ * 8 + j] = p[q];
+  }
+  for (int e = threadIdx.x; e < 2 * 64 * 8; e += 512) {
+    // Q^T A operand: lane (tap, h), k-step m, element j <-> channel crow(8m + j, h)
+    const int j = e & 7, L_ = (e >> 3) & 63, m = e >> 9;
+    const int tap = L_ & 31, c = crow(8 * m + j, L_ >> 5);
+    __bf16 p[3];
+    split3(tap < K3 ? W3[tap * N2 + c] : 0.0f, p[0], p[1], p[2]);
+#pragma unroll
+    for (int q = 0; q < 3; q++) w3i[(m * 3 + q) * 512 + L_ * 8 + j] = p[q];
+  }
+  if (threadIdx.x < 128)
+    a88s[threadIdx.x] = threadIdx.x < 64 ? W1[80 * N1 + threadIdx.x] : B1[threadIdx.x - 64];
+  else if (threadIdx.x < 160)
+    b2i[threadIdx.x - 128] = B2[crow((threadIdx.x - 128) & 15, (threadIdx.x - 128) >> 4)];
+  // Q^T zero columns (never written again)
+  for (int i = threadIdx.x; i < kF6Waves * 25 * 2 * (F3 - 1); i += 512) {
+    const int w = i / (50 * (F3 - 1)), r = (i / (2 * (F3 - 1))) % 25, col = i % (2 * (F3 - 1));
+    qs[(w * 25 + r) * kF6QS + (col < F3 - 1 ? col : kFwdRW + col)] = 0.0f;
+  }
+  __syncthreads();
+  float a88r[NT1];
+#pragma unroll
+  for (int t = 0; t < NT1; t++) a88r[t] = a88s[64 * h + 32 * t + li];
+
+  // L3 window sums (fwd_l123): item k of the F3 x EW (tap row dy, column e) per chunk
+  constexpr int kWin = (F3 * EW + 63) / 64;
+  int wrb[kWin], wwb[kWin];
+#pragma unroll
+  for (int k = 0; k < kWin; k++) {
+    const int it = min(lane + 64 * k, F3 * EW - 1), dy = it / EW, e = it - dy * EW;
+    wrb[k] = (wave * 25 + dy * F3) * kF6QS + e;
+    wwb[k] = (dy * EHM + F3 - 1 - dy) * EW + e;
+  }
+  auto win_read = [&](int k, float* v) {
+#pragma unroll
+    for (int dx = 0; dx < F3; dx++) v[dx] = qs[wrb[k] + dx * (kF6QS + 1)];
+  };
+  auto win_store = [&](int k, const float* v, int pc) {
+    if (k < kWin - 1 || lane + 64 * k < F3 * EW) {
+      float t = 0.0f;
+#pragma unroll
+      for (int dx = 0; dx < F3; dx++) t += v[dx];
+      accs[wwb[k] + pc * EW] = t;
+    }
+  };
+
+  const uint16_t* const wl1 = reinterpret_cast<const uint16_t*>(w1i) + lane * 8;
+  const uint16_t* const wl2 = reinterpret_cast<const uint16_t*>(w2i) + lane * 8;
+  const uint16_t* const wl3 = reinterpret_cast<const uint16_t*>(w3i) + lane * 8;
+  auto w1op = [&](int s_, int t, bf16x8 (&a)[3]) {
+#pragma unroll
+    for (int q = 0; q < 3; q++) a[q] = *reinterpret_cast<const bf16x8*>(wl1 + ((s_ * 2 + t) * 3 + q) * 512);
+  };
+
+  for (int wi = blockIdx.x; wi < n_items; wi += gridDim.x) {
+    const int n = wi / per_frame, rr = wi - n * per_frame;
+    const int ry = rr / g.nrx;
+    const int oy0 = ry * g.rh;
+    const int crh = min(g.rh, g.oh - oy0);
+
+    __syncthreads();  // the previous region's readers are done with the images / accs
+    {
+      uint16_t* const r16 = reinterpret_cast<uint16_t*>(rimg);
+#pragma unroll
+      for (int k = 0; k < kXR; k++) {
+        const int i = threadIdx.x + 512 * k;
+        if (i < TW * kF6XR) {
+          xs[i] = xr[k];
+          __bf16 p[3];
+          split3(xr[k], p[0], p[1], p[2]);
+#pragma unroll
+          for (int q = 0; q < 3; q++) {
+            const uint16_t b = __builtin_bit_cast(uint16_t, p[q]);
+            r16[2 * (q * rn + i)] = b;
+            if (i > 0) r16[2 * (q * rn + i) - 1] = b;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (wi + (int)gridDim.x < n_items) xload(wi + gridDim.x);
+
+    int pc = -1;  // this wave's chunk whose window sums are pending (wave-uniform)
+    float wv[F3];
+    for (int c = wave; c < crh; c += kF6Waves) {  // chunk = region row c, pixel li
+      const int rb = (c + h) * TW + li;
+      const int b4 = h ? c * TW + li + 8 : (c + 8) * TW + li, st4 = h ? TW : 1;
+      f32x16 acc1[NT1];
+      {
+        const float bx = h ? 1.0f : xs[(c + 8) * TW + li + 8];
+#pragma unroll
+        for (int t = 0; t < NT1; t++) acc1[t] = mma(a88r[t], bx, zero16());
+      }
+      auto xop = [&](int s_, bf16x8 (&b)[3]) {
+#pragma unroll
+        for (int q = 0; q < 3; q++) {
+          const uint32_t* r = rimg + q * rn + rb + 2 * s_ * TW;
+          u32x4 d;
+          d[0] = r[0];
+          d[1] = r[2];
+          d[2] = r[4];
+          d[3] = r[6];
+          b[q] = __builtin_bit_cast(bf16x8, d);
+        }
+      };
+      bf16x8 wa[2][3], xb[2][3];
+      float x4[8];
+      xop(0, xb[0]);
+      w1op(0, 0, wa[0]);
+#pragma unroll
+      for (int gi = 0; gi < 10; gi++) {
+        const int s_ = gi >> 1, t = gi & 1;
+        if (gi + 1 < 10) w1op((gi + 1) >> 1, (gi + 1) & 1, wa[(gi + 1) & 1]);
+        if (t == 0 && s_ + 1 < 4) xop(s_ + 1, xb[(s_ + 1) & 1]);
+        if (gi == 4) {
+#pragma unroll
+          for (int j = 0; j < 8; j++) x4[j] = xs[b4 + j * st4];
+        }
+        if (gi == 6) split8(x4, xb[0]);
+        // the previous chunk's window sums ride in this stream
+        if (pc >= 0 && (gi & 1) && (gi >> 1) < kWin) win_read(gi >> 1, wv);
+        __builtin_amdgcn_sched_barrier(0);
+        acc1[t] = mma_x6(wa[gi & 1], xb[s_ & 1], acc1[t]);
+        if (pc >= 0 && gi >= 2 && !(gi & 1) && (gi >> 1) - 1 < kWin) win_store((gi >> 1) - 1, wv, pc);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int t = 0; t < NT1; t++)
+#pragma unroll
+        for (int r = 0; r < 16; r++) acc1[t][r] = relu1(acc1[t][r]);
+      f32x16 acc2;
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const mfma::f32x4 v_ = *reinterpret_cast<const mfma::f32x4*>(&b2i[16 * h + 4 * q]);
+#pragma unroll
+        for (int e = 0; e < 4; e++) acc2[4 * q + e] = v_[e];
+      }
+      auto opsplit = [&](const f32x16& acc, int m, bf16x8 (&b)[3]) {
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) v[j] = acc[8 * (m & 1) + j];
+        split8(v, b);
+      };
+      bf16x8 wb[2][3], bb[2][3];
+      auto wop = [&](const uint16_t* wl, int m, bf16x8 (&a)[3]) {
+#pragma unroll
+        for (int q = 0; q < 3; q++) a[q] = *reinterpret_cast<const bf16x8*>(wl + (m * 3 + q) * 512);
+      };
+      wop(wl2, 0, wb[0]);
+      opsplit(acc1[0], 0, bb[0]);
+#pragma unroll
+      for (int m = 0; m < 4; m++) {
+        if (m + 1 < 4) wop(wl2, m + 1, wb[(m + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+        acc2 = mma_x6(wb[m & 1], bb[m & 1], acc2);
+        if (m + 1 < 4) opsplit(acc1[(m + 1) >> 1], m + 1, bb[(m + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; r++) acc2[r] = relu1(acc2[r]);
+      // Q^T[tap][p] = sum_c W3[tap][c] A2^T[c][p]
+      f32x16 accq = zero16();
+      wop(wl3, 0, wb[0]);
+      opsplit(acc2, 0, bb[0]);
+#pragma unroll
+      for (int m = 0; m < 2; m++) {
+        if (m + 1 < 2) {
+          wop(wl3, 1, wb[1]);
+          opsplit(acc2, 1, bb[1]);
+        }
+        accq = mma_x6(wb[m], bb[m], accq);
+      }
+      // Q^T rows (taps) crow(r, h) < 25 of pixel li (the pending window sums
+      // above read the previous Q^T: their values are summed by now)
+#pragma unroll
+      for (int r = 0; r < 16; r++)
+        if (crow(r, h) < K3) qs[(wave * 25 + crow(r, h)) * kF6QS + li + F3 - 1] = accq[r];
+      __builtin_amdgcn_wave_barrier();
+      pc = c;
+    }
+    if (pc >= 0) {
+#pragma unroll
+      for (int k = 0; k < kWin; k++) {
+        win_read(k, wv);
+        win_store(k, wv, pc);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    float* dst = part + (size_t)wi * EH * EW;
+    for (int i = threadIdx.x; i < EH * EW; i += 512) {
+      const int pr = i / EW, e = i - pr * EW;
+      float v = 0.0f;
+#pragma unroll
+      for (int dy = 0; dy < F3; dy++) {
+        const int c = pr - (F3 - 1) + dy;
+        if (c >= 0 && c < crh) v += accs[(dy * EHM + pr) * EW + e];
+      }
+      dst[i] = v;
+    }
+  }
+  SRCNN_CLOCK_END(g_clk_fwd, 0);
+}
+
 // A3[y][x] = B3 + the partials of the regions (ry, rx) in {y, y+f3-1}/rh x
 // {x, x+f3-1}/32 (ConfigBasedDataPipeline.cpp:224-238, last layer: no ReLU).
 // Grid (columns / blockDim.x, rows, frames): the row's region range is block
@@ -330,9 +630,11 @@ int run_forward(const float* X, uint32_t w, uint32_t h, uint32_t batch, const fl
                 size_t* need) {
   const int ow = (int)w - F1 + 1, oh = (int)h - F1 + 1;
   if (ow < F3 || oh < F3) return 0;
+  // the default net in split-bf16 products (fwd_l123x6), fixed 24-row regions
+  const bool x6 = N1 == 64 && N2 == 32 && F1 == 9 && F3 == 5 && g_arith == 0;
   // region rows: the input tile (32 + f1 - 1) x (rh + f1 - 1) fits the LDS tile,
   // a multiple of the 4 waves
-  int rh = std::min((kFwdXs / (kFwdRW + F1 - 1) - (F1 - 1)) / 4 * 4, kFwdRhMax / 4 * 4);
+  int rh = x6 ? kF6Rh : std::min((kFwdXs / (kFwdRW + F1 - 1) - (F1 - 1)) / 4 * 4, kFwdRhMax / 4 * 4);
   if (rh < F3) return 0;
   rh = std::min(rh, oh);
   FwdGeom g{(int)w, (int)h, ow, oh, rh, (ow + kFwdRW - 1) / kFwdRW, (oh + rh - 1) / rh, (int)batch};
@@ -353,8 +655,16 @@ int run_forward(const float* X, uint32_t w, uint32_t h, uint32_t batch, const fl
   const float* B3 = W3 + F3 * F3 * N2;
   {
     SRCNN_PROFILE("fwd_l123_mfma", s);
-    hipLaunchKernelGGL((fwd_l123_kernel<N1, N2, F1, F3>), dim3((unsigned)std::min<long>(items, kFwdGrid)),
-                       dim3(256), 0, s, X, W1, B1, W2, B2, W3, part, g);
+    if (x6) {
+      hipError_t e = hipFuncSetAttribute((const void*)fwd_l123x6_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         160 * 1024);
+      if (e != hipSuccess) return fail(SRCNN_ERR_HIP, "hipFuncSetAttribute(fwd_l123x6): %s", hipGetErrorString(e));
+      hipLaunchKernelGGL(fwd_l123x6_kernel, dim3((unsigned)std::min<long>(items, 256)), dim3(512), F6Lds::bytes, s,
+                         X, W1, B1, W2, B2, W3, part, g);
+    } else {
+      hipLaunchKernelGGL((fwd_l123_kernel<N1, N2, F1, F3>), dim3((unsigned)std::min<long>(items, kFwdGrid)),
+                         dim3(256), 0, s, X, W1, B1, W2, B2, W3, part, g);
+    }
     SRCNN_LAUNCH_TRY();
   }
   {
@@ -386,8 +696,9 @@ int preload_forward(const srcnn_net* net) {
   if (net->f2 != 1) return 0;
 #define SRCNN_FWD_CASE(A, B, C, D)                                                        \
   if (net->n1 == A && net->n2 == B && net->f1 == C && net->f3 == D) {                    \
-    const void* k[] = {(const void*)fwd_l123_kernel<A, B, C, D>, (const void*)fwd_seam_kernel<D>}; \
-    int rc = resolve_kernels(k, 2);                                                      \
+    const void* k[] = {(const void*)fwd_l123_kernel<A, B, C, D>, (const void*)fwd_seam_kernel<D>, \
+                       (const void*)fwd_l123x6_kernel};                                  \
+    int rc = resolve_kernels(k, A == 64 && B == 32 ? 3 : 2);                             \
     return rc ? rc : 1;                                                                  \
   }
   SRCNN_FWD_CASE(64, 32, 9, 5)

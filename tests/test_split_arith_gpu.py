@@ -76,3 +76,28 @@ def test_split_arith_within_fp32_error(S, batch, size, sd):
                     "err_split": es, "err_f32_mfma": ef, "err_f32_oracle": eo})
         print("%s batch %d: split %.3e  fp32 MFMA %.3e  fp32 oracle %.3e" % (nm, batch, es, ef, eo))
         assert es <= 1.5 * ef + 2.0 ** -24, (nm, es, ef)
+
+
+@pytest.mark.parametrize("w,h", [(256, 256), (333, 197)])
+def test_split_forward_within_fp32_error(S, w, h):
+    """The inference path (fwd_l123x6 vs fwd_l123) likewise."""
+    rng = np.random.default_rng(11)
+    X = (rng.random(w * h, dtype=np.float32) - 0.5).astype(np.float32)
+    params = make_params(rng, NET, sd=0.05)
+    ref64 = orc.f64.forward(NET, X, w, h, 1, params)
+    ref32 = orc.forward(NET, X, w, h, 1, params)
+    net = S.Net(*NET)
+    errs = {}
+    for arith in (0, 1):
+        S.set_arith(arith)
+        # (the split kernel's regions are 24 rows, the fp32 one's 28: query per arithmetic)
+        nbytes = S.forward_workspace_bytes(net, w, h, 1)
+        ws = torch.empty(nbytes // 4 + 64, dtype=torch.float32, device="cuda")
+        out = torch.empty(ref32.size, dtype=torch.float32, device="cuda")
+        S.forward(net, D(X), w, h, 1, D(params), out, ws, nbytes)
+        errs[arith] = normwise(H(out), ref64)
+    log_record({"test": "split_forward", "w": w, "h": h, "err_split": errs[0], "err_f32_mfma": errs[1],
+                "err_f32_oracle": normwise(ref32, ref64)})
+    print("forward %dx%d: split %.3e  fp32 MFMA %.3e  fp32 oracle %.3e"
+          % (w, h, errs[0], errs[1], normwise(ref32, ref64)))
+    assert errs[0] <= 1.5 * errs[1] + 2.0 ** -24, errs
