@@ -639,7 +639,16 @@ int run_forward(const float* X, uint32_t w, uint32_t h, uint32_t batch, const fl
   rh = std::min(rh, oh);
   FwdGeom g{(int)w, (int)h, ow, oh, rh, (ow + kFwdRW - 1) / kFwdRW, (oh + rh - 1) / rh, (int)batch};
   const long items = (long)g.batch * g.nrx * g.nry;
-  const size_t pbytes = (size_t)items * (rh + F3 - 1) * (kFwdRW + F3 - 1) * sizeof(float);
+  // partial sums of either arithmetic's regions (srcnn_set_arith between the
+  // size query and the call needs no new query)
+  auto part_bytes = [&](int r) {
+    return (size_t)g.batch * g.nrx * ((oh + r - 1) / r) * (r + F3 - 1) * (kFwdRW + F3 - 1) * sizeof(float);
+  };
+  size_t pbytes = part_bytes(rh);
+  if (N1 == 64 && N2 == 32 && F1 == 9 && F3 == 5) {
+    const int rh_f32 = std::min(std::min((kFwdXs / (kFwdRW + F1 - 1) - (F1 - 1)) / 4 * 4, kFwdRhMax / 4 * 4), oh);
+    pbytes = std::max({pbytes, part_bytes(rh_f32), part_bytes(std::min(kF6Rh, oh))});
+  }
   if (query_only) {
     *need = pbytes;
     return 1;
