@@ -98,53 +98,78 @@ __global__ __launch_bounds__(256, 2) void l12x6_fwd_kernel(const float* __restri
   if ((int)blockIdx.x < g.batch) xload(blockIdx.x);
 
   // ---- split operand images of W1 / W2 (with the pending update folded in) ----
+  // Each thread takes 4 consecutive parameters per 16-B load (W1 taps 0-79:
+  // 5 loads, W2: 2 loads; with the lazy update the same from P, M and G, all
+  // in flight at once) and scatters their parts into the images.
   if constexpr (kLazy) lazy_write_slice(lz);
   auto prm = [&](int seg, int i) -> float {
     if constexpr (kLazy) return lazy_param(lz, seg, i);
     return (seg == 0 ? W1 : seg == 1 ? B1 : seg == 2 ? W2 : B2)[i];
   };
-  {
-    // W1: element e = (s, t, lane, j); every tap but (8, 8) exactly once
-    constexpr int kN = kX6KS * 2 * 64 * 8, kIt = kN / 256;
-    float v[kIt];
-#pragma unroll
-    for (int k = 0; k < kIt; k++) {
-      const int e = threadIdx.x + 256 * k;
-      const int j = e & 7, L_ = (e >> 3) & 63, t = (e >> 9) & 1, s = e >> 10;
-      const int gg = 2 * s + (L_ >> 5);
-      const int tap = gg <= 8 ? gg * F1 + j : j * F1 + 8;
-      v[k] = prm(0, tap * N1 + 32 * t + (L_ & 31));
+  // 4 consecutive parameters of segment seg from index i (16-B aligned)
+  auto prm4 = [&](int seg, int i, f32x4& v, f32x4& m, f32x4& gr) {
+    if constexpr (kLazy) {
+      const uint32_t gi = lz.off[seg] + i;
+      v = *reinterpret_cast<const f32x4*>(lz.P + gi);
+      m = *reinterpret_cast<const f32x4*>(lz.M + gi);
+      gr = *reinterpret_cast<const f32x4*>(lz.G + gi);
+    } else {
+      v = *reinterpret_cast<const f32x4*>((seg == 0 ? W1 : W2) + i);
     }
+  };
+  auto upd4 = [&](int seg, f32x4& v, f32x4& m, const f32x4& gr) {
+    if constexpr (kLazy) {
 #pragma unroll
-    for (int k = 0; k < kIt; k++) {
-      const int e = threadIdx.x + 256 * k;
-      const int j = e & 7, L_ = (e >> 3) & 63, t = (e >> 9) & 1, s = e >> 10;
-      __bf16 p[3];
-      split3(v[k], p[0], p[1], p[2]);
+      for (int e = 0; e < 4; e++) {
+        float w_ = v[e], m_ = m[e];
+        sgd_step(w_, m_, seg, gr[e], lz.lr[seg >> 1], lz.mu, lz.wd, lz.batch);
+        v[e] = w_;
+      }
+    }
+  };
+  {
+    // W1 taps 0-79 (5120 parameters, 5 quads per thread): parameter tap * 64
+    // + ch sits at k-step s, tile ch / 32, lane (ch % 32) + 32 h, element j
+    // with (g = 2s + h, j) = (dy, dx) for dx < 8, (9, dy) for dx = 8
+    constexpr int kQ = 5120 / 4 / 256;
+    f32x4 v[kQ], m[kQ], gr[kQ];
 #pragma unroll
-      for (int q = 0; q < 3; q++) w1i[((s * 2 + t) * 3 + q) * 512 + L_ * 8 + j] = p[q];
+    for (int k = 0; k < kQ; k++) prm4(0, 4 * (threadIdx.x + 256 * k), v[k], m[k], gr[k]);
+#pragma unroll
+    for (int k = 0; k < kQ; k++) {
+      upd4(0, v[k], m[k], gr[k]);
+      const int p0 = 4 * (threadIdx.x + 256 * k), tap = p0 >> 6, dy = tap / F1, dx = tap - dy * F1;
+      const int gg = dx < 8 ? dy : 9, j = dx < 8 ? dx : dy, s_ = gg >> 1, hh = gg & 1;
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        const int ch = (p0 & 63) + e, t = ch >> 5, L_ = (ch & 31) + 32 * hh;
+        __bf16 p[3];
+        split3(v[k][e], p[0], p[1], p[2]);
+#pragma unroll
+        for (int q = 0; q < 3; q++) w1i[((s_ * 2 + t) * 3 + q) * 512 + L_ * 8 + j] = p[q];
+      }
     }
   }
   {
-    // W2^T as the L2 A operand: k-step m, lane (n, h), element j <-> channel
-    // 32 (m >> 1) + crow(8 (m & 1) + j, h)
-    constexpr int kN = 4 * 64 * 8, kIt = kN / 256;
-    float v[kIt];
+    // W2 (2048 parameters, 2 quads per thread): parameter c * 32 + n sits at
+    // k-step m, lane n + 32 h, element j with c = 32 (m >> 1) + crow(8 (m & 1) + j, h)
+    constexpr int kQ = 2048 / 4 / 256;
+    f32x4 v[kQ], m[kQ], gr[kQ];
 #pragma unroll
-    for (int k = 0; k < kIt; k++) {
-      const int e = threadIdx.x + 256 * k;
-      const int j = e & 7, L_ = (e >> 3) & 63, m = e >> 9;
-      const int c = 32 * (m >> 1) + crow(8 * (m & 1) + j, L_ >> 5);
-      v[k] = prm(2, c * N2 + (L_ & 31));
-    }
+    for (int k = 0; k < kQ; k++) prm4(2, 4 * (threadIdx.x + 256 * k), v[k], m[k], gr[k]);
 #pragma unroll
-    for (int k = 0; k < kIt; k++) {
-      const int e = threadIdx.x + 256 * k;
-      const int j = e & 7, L_ = (e >> 3) & 63, m = e >> 9;
-      __bf16 p[3];
-      split3(v[k], p[0], p[1], p[2]);
+    for (int k = 0; k < kQ; k++) {
+      upd4(2, v[k], m[k], gr[k]);
+      const int p0 = 4 * (threadIdx.x + 256 * k), c = p0 >> 5, r = c & 31;
+      const int hh = (r >> 2) & 1, rr = (r & 3) + 4 * (r >> 3), mm = 2 * (c >> 5) + (rr >> 3), j = rr & 7;
 #pragma unroll
-      for (int q = 0; q < 3; q++) w2i[(m * 3 + q) * 512 + L_ * 8 + j] = p[q];
+      for (int e = 0; e < 4; e++) {
+        const int L_ = (p0 & 31) + e + 32 * hh;
+        __bf16 p[3];
+        split3(v[k][e], p[0], p[1], p[2]);
+#pragma unroll
+        for (int q = 0; q < 3; q++) w2i[(mm * 3 + q) * 512 + L_ * 8 + j] = p[q];
+      }
     }
   }
   if (threadIdx.x < 128)
