@@ -23,8 +23,10 @@
 //                  one ds_read2_b32 per run and part from part-interleaved
 //                  pair images (row runs: R; column runs: T, column-major)
 //   gB2[n] += sum_p delta2[p][n]                     VALU over delta2^T
-// Each wave accumulates over its chunks and writes its own slab (no block
-// reduction; 4 slabs per block, summed by slab_reduce in block order).
+// Each wave accumulates over its chunks; at the end the four waves' sums are
+// added in wave order through LDS and the block writes one slab (summed by
+// slab_reduce in block order).  (One slab per wave was 4x the slab traffic:
+// 30 MB written and read back per step.)
 // One wave per SIMD (512 registers: 128 accumulators + operands).
 
 constexpr int kD6W2 = 2 * 2 * 3 * 512;  // delta1's W2 image, bf16: [t][k][part][lane][8]
@@ -335,8 +337,40 @@ __global__ __launch_bounds__(256, 1) void d1x6_grad12_kernel(const float* __rest
   }
   SRCNN_CLOCK_END(g_clk, 2);
 
-  // ---- this wave's slab: [gW1 | gB1 | gW2 | gB2] ----
-  float* out = slab + ((size_t)blockIdx.x * 4 + wave) * P12;
+  // ---- block reduction: waves 1-3 hand their accumulators to wave 0 one
+  // 16-register tile at a time, added in wave order (fixed, deterministic) ----
+  __syncthreads();  // every wave is done with the LDS images
+  float* const red = smem;  // [3 waves][16 registers][64 lanes]
+  auto reduce_tile = [&](f32x16& acc) {
+    if (wave > 0) {
+#pragma unroll
+      for (int r = 0; r < 16; r++) red[((wave - 1) * 16 + r) * 64 + lane] = acc[r];
+    }
+    __syncthreads();
+    if (wave == 0) {
+#pragma unroll
+      for (int w = 0; w < 3; w++)
+#pragma unroll
+        for (int r = 0; r < 16; r++) acc[r] += red[(w * 16 + r) * 64 + lane];
+    }
+    __syncthreads();
+  };
+#pragma unroll
+  for (int t = 0; t < 2; t++) {
+#pragma unroll
+    for (int u = 0; u < 3; u++) reduce_tile(g1[t][u]);
+    reduce_tile(g2[t]);
+  }
+  if (wave > 0) red[(wave - 1) * 64 + lane] = gb2;
+  __syncthreads();
+  if (wave == 0) {
+#pragma unroll
+    for (int w = 0; w < 3; w++) gb2 += red[w * 64 + lane];
+  }
+  if (wave != 0) return;
+
+  // ---- the block's slab: [gW1 | gB1 | gW2 | gB2] ----
+  float* out = slab + (size_t)blockIdx.x * P12;
 #pragma unroll
   for (int t = 0; t < 2; t++)
 #pragma unroll

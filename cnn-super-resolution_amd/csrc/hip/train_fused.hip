@@ -999,12 +999,12 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   int d1c_parts = kD1c ? std::max(1, std::min({4, nch1, kD1cGrid / (int)std::max<uint32_t>(batch, 1)})) : 1;
   while (d1c_parts > 1 && (d1c_parts - 1) * ((nch1 + d1c_parts - 1) / d1c_parts) >= nch1)
     d1c_parts--;  // every part holds at least one chunk (the kernel's DMA pipeline assumes it)
-  const int gd6 = grid_for_batch(batch, 256);  // d1x6: 4 slabs (waves) per block
+  const int gd6 = grid_for_batch(batch, 256);  // d1x6: one slab per block
   const int gdf = kD1c ? (int)std::min<size_t>((size_t)batch * d1c_parts, kD1cGrid) : grid_for_batch(batch, 512);
-  const int gd = x6 ? 4 * gd6 : gdf;
+  const int gd = x6 ? gd6 : gdf;
   // (the workspace holds either arithmetic's slabs: srcnn_set_arith between
   // the size query and the step needs no new query)
-  const size_t s12 = (size_t)std::max(4 * gd6, gdf) * NetT::P12;
+  const size_t s12 = (size_t)std::max(gd6, gdf) * NetT::P12;
   size_t s3 = (size_t)g3 * NetT::P3, ssq = g3;  // gW3 slabs, squared-error slabs
   if (!l3_fused) {  // the op-level gW3 slabs; the same space serves the squared-error reduction
     s3 = fast::grad_workspace_bytes(N2, 1, F3, w3, h3, batch) / sizeof(float);
