@@ -35,6 +35,7 @@ constexpr int kD6Sc = 32 * 36;           // per-wave delta2 transpose scratch (f
 struct D6Lds {
   int st;      // T image column stride (dwords per column, >= 4 cr + 9)
   int tcols;   // T image columns (the column runs' x range + 8)
+  int rs;      // R image row stride (pixels): the least >= w with rs = 9 (mod 64)
   int rdw;     // R image dwords (3 parts interleaved)
   int tdw;     // T image dwords
   int xbuf;    // one X buffer (dwords): R then T
@@ -43,7 +44,12 @@ struct D6Lds {
     st = 4 * rg.cr + 9;
     if (st < h + 1) st = h + 1;
     tcols = rg.b ? rg.b + 8 : 0;
-    rdw = 3 * (w * h + 1);
+    // a tap (dy, dx) of gW1's X operand sits 3 (dy rs + dx) dwords past its
+    // run base, = 3 (9 dy + dx) = 3 tap (mod 64) for rs = 9 (mod 64): the 32
+    // taps of a half-wave hit 32 distinct banks (at rs = w = 33 two taps
+    // shared a bank: 53% of d1x6's LDS-active cycles were bank conflicts)
+    rs = w + ((9 - w) % 64 + 64) % 64;
+    rdw = 3 * (rs * h + 1);
     tdw = 3 * tcols * st;
     xbuf = rdw + tdw;
     w2 = 0;
@@ -99,12 +105,13 @@ __global__ __launch_bounds__(256, 1) void d1x6_grad12_kernel(const float* __rest
     int iy, ix;
     bool col;
     run_origin(rg, k < rg.nrun ? k : 0, iy, ix, col);
-    runs[k] = col ? ~(L.rdw + 3 * ((ix - x0col) * L.st + iy)) : 3 * (iy * W + ix);
+    runs[k] = col ? ~(L.rdw + 3 * ((ix - x0col) * L.st + iy)) : 3 * (iy * L.rs + ix);
   }
-  // T rows past the tile (and the pair partner of the last row) stay zero
-  for (int i = threadIdx.x; i < L.tdw; i += 256) {
-    xbuf[L.rdw + i] = 0u;
-    xbuf[L.xbuf + L.rdw + i] = 0u;
+  // T rows past the tile (and the pair partner of the last row), and the R
+  // rows' pad columns, stay zero
+  for (int i = threadIdx.x; i < L.xbuf; i += 256) {
+    xbuf[i] = 0u;
+    xbuf[L.xbuf + i] = 0u;
   }
   {
     // delta1's B operand W2^T: tile t, k-step k, lane (c, h), element j <->
@@ -134,7 +141,7 @@ __global__ __launch_bounds__(256, 1) void d1x6_grad12_kernel(const float* __rest
   for (int u = 0; u < 3; u++) {
     const int tap = 32 * u + li;
     const int dy = tap < K1 ? tap / F1 : 0, dx = tap < K1 ? tap - dy * F1 : 0;
-    offR3[u] = 3 * (dy * W + dx);
+    offR3[u] = 3 * (dy * L.rs + dx);
     offT3[u] = 3 * (dx * L.st + dy);
   }
   const bool ones = li == K1 - 64;  // tile 2: tap 81 is the ones column (gB1)
@@ -195,13 +202,13 @@ __global__ __launch_bounds__(256, 1) void d1x6_grad12_kernel(const float* __rest
         if (i < xn) {
           __bf16 p[3];
           split3(xr[k], p[0], p[1], p[2]);
-          const int y = i / W, x = i - y * W;
+          const int y = i / W, x = i - y * W, ri = y * L.rs + x;
           const int ti = L.rdw + 3 * ((x - x0col) * L.st + y);
 #pragma unroll
           for (int q = 0; q < 3; q++) {
             const uint16_t b = __builtin_bit_cast(uint16_t, p[q]);
-            x16[2 * (3 * i + q)] = b;
-            if (i > 0) x16[2 * (3 * (i - 1) + q) + 1] = b;
+            x16[2 * (3 * ri + q)] = b;
+            if (ri > 0) x16[2 * (3 * (ri - 1) + q) + 1] = b;
             if (L.tcols && x >= x0col) {
               x16[2 * (ti + q)] = b;
               if (y > 0) x16[2 * (ti - 3 + q) + 1] = b;

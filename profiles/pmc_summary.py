@@ -19,6 +19,9 @@ from collections import defaultdict
 
 SHORT = [
     (r"l12_fwd_kernel", "l12_fwd_mfma"),
+    (r"l12x6_fwd_kernel", "l12_fwd_mfma"),
+    (r"d1x6_grad12_kernel", "delta1_grad12_fused"),
+    (r"fwd_l123x6_kernel", "fwd_l123_mfma"),
     (r"l3_delta_kernel", "l3_delta_fused"),
     (r"l3r_delta_kernel", "l3_delta_fused"),
     (r"d1_grad12_kernel", "delta1_grad12_fused"),
