@@ -30,6 +30,7 @@
 #include "common.hpp"
 #include "mfma.hpp"
 #include "ops.hpp"
+#include "split.hpp"
 
 // M0 is written only by the LDS-DMA asm below (nothing else in this file uses it)
 #pragma clang diagnostic ignored "-Winline-asm"
@@ -439,6 +440,152 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(const float* __restri
               out[idx] = fmaxf(acc[m][r] + bn, 0.0f);
           }
         }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// wl2x6: the L2 forward of the step (conv_mfma_kernel<.., false> over the
+// whole image) with its products in split-bf16 form (split.hpp): per tap and
+// 16-channel chunk ONE 32x32x16 k-step of six part products instead of 8
+// fp32 32x32x2 MFMAs (6 x 32 against 8 x 64 matrix cycles).
+//   A: the chunk's image split once into LDS, [pixel][part][16 ch] bf16 rows
+//      of 112 B (16-lane groups of ds_read_b128 conflict-free); lane (pixel
+//      j, half h) reads channels 8h .. 8h+7 of each part: 3 ds_read_b128
+//   B: W2 split by wprep_w2x6_kernel into [nt][chunk][tap][part][lane][8]
+//      bf16, lane (n, h) holding W2[tap][16 chunk + 8h + i][32 nt + n]
+// The next chunk is register-staged (16-B global loads issued at the chunk's
+// start) and split into the other image after the chunk's MFMAs: one barrier
+// per chunk, no LDS-DMA.  Same work split, C layout and epilogue as conv_mfma.
+// ---------------------------------------------------------------------------
+constexpr int kW6Row = 28;  // dwords per staged pixel: 3 parts x 16 bf16 + 16 B pad
+// pixels of one chunk image: two images in the 160 KiB LDS
+constexpr int kW6ImgMax = 160 * 1024 / (2 * kW6Row * 4);
+
+template <int CIN, int COUT, int F>
+__global__ void wprep_w2x6_kernel(const float* __restrict__ W2, uint16_t* __restrict__ Wx) {
+  constexpr int NCH = CIN / 16, FF = F * F, NT = COUT / 32;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= NT * NCH * FF * 64 * 8) return;
+  const int i = e & 7, L = (e >> 3) & 63, rest = e >> 9;
+  const int t = rest % FF, c = (rest / FF) % NCH, nt = rest / (FF * NCH);
+  const int ch = 16 * c + 8 * (L >> 5) + i, n = 32 * nt + (L & 31);
+  __bf16 p[3];
+  mfma::split3(W2[((size_t)t * CIN + ch) * COUT + n], p[0], p[1], p[2]);
+#pragma unroll
+  for (int q = 0; q < 3; q++) Wx[((size_t)rest * 3 + q) * 512 + L * 8 + i] = __builtin_bit_cast(uint16_t, p[q]);
+}
+
+template <int CIN, int COUT, int F, int MT>
+__global__ __launch_bounds__(256, 1) void wl2x6_fwd_kernel(const float* __restrict__ in,
+                                                          const uint16_t* __restrict__ Wx,
+                                                          const float* __restrict__ bias,
+                                                          float* __restrict__ out, CGeom g) {
+  using mfma::bf16x8;
+  constexpr int NCH = CIN / 16, FF = F * F;
+  static_assert(CIN % 16 == 0 && COUT == 64, "one 64-channel part");
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int lane = lane_id(), wave = wave_id(), j = lane & 31, h = lane >> 5;
+  const int nt = wave & 1, mg = wave >> 1;
+  const int ipx = g.img_w * g.img_h, npx = g.npx;
+  uint32_t* const img0 = reinterpret_cast<uint32_t*>(smem);
+  uint32_t* const img1 = img0 + ipx * kW6Row;
+  // register staging of one chunk: quad i = pixel i / 4, channels 4 (i % 4) ..
+  constexpr int kQ = (kW6ImgMax * 4 + 255) / 256;
+  f32x4 xr[kQ];
+  auto load = [&](int s, int c) __attribute__((always_inline)) {
+    const float* src = in + (size_t)s * ipx * CIN + 16 * c;
+#pragma unroll
+    for (int k = 0; k < kQ; k++) {
+      const int i = threadIdx.x + 256 * k;
+      if (i < ipx * 4) xr[k] = *reinterpret_cast<const f32x4*>(src + (size_t)(i >> 2) * CIN + 4 * (i & 3));
+    }
+  };
+  auto store_split = [&](uint32_t* buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < kQ; k++) {
+      const int i = threadIdx.x + 256 * k;
+      if (i < ipx * 4) {
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 4; e++) v[e] = v[4 + e] = xr[k][e];
+        bf16x8 pp[3];
+        mfma::split8(v, pp);
+        uint32_t* d = buf + (i >> 2) * kW6Row + 2 * (i & 3);
+#pragma unroll
+        for (int q = 0; q < 3; q++) {
+          const mfma::u32x4 w = __builtin_bit_cast(mfma::u32x4, pp[q]);
+          *reinterpret_cast<uint2*>(d + 8 * q) = make_uint2(w[0], w[1]);
+        }
+      }
+    }
+  };
+  const int nitems = g.batch;
+  if ((int)blockIdx.x < nitems) {
+    load(blockIdx.x, 0);
+    store_split(img0);
+  }
+  __syncthreads();
+  int phase = 0;
+  for (int it = blockIdx.x; it < nitems; it += gridDim.x) {
+    const int s = it;
+    int abase[MT];
+#pragma unroll
+    for (int m = 0; m < MT; m++) {
+      const int o = min(32 * (2 * m + mg) + j, npx - 1), oy = o / g.out_w;
+      abase[m] = (oy * g.img_w + o - oy * g.out_w) * kW6Row + 4 * h;
+    }
+    f32x16 acc[MT];
+#pragma unroll
+    for (int m = 0; m < MT; m++) acc[m] = zero16();
+    const uint16_t* wl = Wx + (size_t)nt * NCH * FF * 3 * 512 + lane * 8;
+    for (int c = 0; c < NCH; c++) {
+      const uint32_t* cur = phase ? img1 : img0;
+      uint32_t* nxt = phase ? img0 : img1;
+      const int ns = c + 1 < NCH ? s : s + (int)gridDim.x, nc = c + 1 < NCH ? c + 1 : 0;
+      const bool more = ns < nitems;
+      if (more) load(ns, nc);
+      const uint16_t* wc = wl + (size_t)c * FF * 3 * 512;
+      // B operands: this tap's, and the next tap's loaded under its MFMAs
+      bf16x8 bq[3], bn[3];
+#pragma unroll
+      for (int q = 0; q < 3; q++) bq[q] = *reinterpret_cast<const bf16x8*>(wc + q * 512);
+#pragma unroll 1
+      for (int dy = 0; dy < F; dy++) {
+#pragma unroll
+        for (int dx = 0; dx < F; dx++) {
+          const int t = dy * F + dx, tn = min(t + 1, FF - 1);
+#pragma unroll
+          for (int q = 0; q < 3; q++) bn[q] = *reinterpret_cast<const bf16x8*>(wc + (tn * 3 + q) * 512);
+          const int toff = (dy * g.img_w + dx) * kW6Row;
+#pragma unroll
+          for (int m = 0; m < MT; m++) {
+            bf16x8 a[3];
+#pragma unroll
+            for (int q = 0; q < 3; q++) a[q] = *reinterpret_cast<const bf16x8*>(cur + abase[m] + toff + 8 * q);
+            acc[m] = mfma::mma_x6(a, bq, acc[m]);
+          }
+#pragma unroll
+          for (int q = 0; q < 3; q++) bq[q] = bn[q];
+        }
+      }
+      if (more) store_split(nxt);
+      __syncthreads();
+      phase ^= 1;
+    }
+    const int n = nt * 32 + j;
+    const float bn = bias[n];
+    const size_t obase = (size_t)s * npx * COUT + n;
+#pragma unroll
+    for (int m = 0; m < MT; m++) {
+      int hl = h;
+      asm volatile("" : "+v"(hl));
+      const int p0 = 32 * (2 * m + mg) + 4 * hl;
+#pragma unroll
+      for (int r = 0; r < 16; r++) {
+        const int pix = p0 + crow(r, 0);
+        if (pix < npx) out[obase + (size_t)pix * COUT] = fmaxf(acc[m][r] + bn, 0.0f);
       }
     }
   }
@@ -1400,11 +1547,14 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   const int G3 = (int)std::min<uint32_t>(batch, wl3l ? 256 : 512);  // all blocks resident
   const int GC = 256;
   const int G2 = g2.groups * (N1 / 32);
-  // workspace: Wf | Wd | slab1 | slab2 | slab3 | sqs
-  const size_t nWf = align_f(NetT::W2), nWd = align_f(NetT::W2);
+  // workspace: Wf | Wd | Wx (split W2 image, wl2x6) | slab1 | slab2 | slab3 | sqs
+  const size_t nWf = align_f(NetT::W2), nWd = align_f(NetT::W2), nWx = align_f((size_t)NetT::W2 * 3 / 2);
+  // the split-bf16 L2 forward (wl2x6): two split chunk images in LDS
+  const size_t lds6 = 2 * (size_t)cf.img_w * cf.img_h * kW6Row * sizeof(float);
+  const bool x6 = g_arith == 0 && N2 == 64 && N1 % 16 == 0 && cf.img_w * cf.img_h <= kW6ImgMax;
   const size_t n1 = align_f((size_t)G1 * NetT::P1), n2 = align_f((size_t)g2.groups * NetT::P2);
   const size_t n3 = align_f((size_t)G3 * NetT::P3), nsq = align_f(G3);
-  const size_t bytes = (nWf + nWd + n1 + n2 + n3 + nsq) * sizeof(float);
+  const size_t bytes = (nWf + nWd + nWx + n1 + n2 + n3 + nsq) * sizeof(float);
   if (query_only) {
     *need = bytes;
     return 1;
@@ -1413,7 +1563,8 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
     return fail(SRCNN_ERR_WORKSPACE, "wide train step: workspace %zu B < %zu B", slab_bytes, bytes);
   float* Wf = slab;
   float* Wd = Wf + nWf;
-  float* slab1 = Wd + nWd;
+  uint16_t* Wx = reinterpret_cast<uint16_t*>(Wd + nWd);
+  float* slab1 = Wd + nWd + nWx;
   float* slab2 = slab1 + n1;
   float* slab3 = slab2 + n2;
   float* sqs = slab3 + n3;
@@ -1429,6 +1580,11 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
     hipLaunchKernelGGL((prepack_w2_kernel<N1, N2, F2, true>), dim3((tot + 255) / 256), dim3(256), 0, s,
                        W2, Wf, Wd);
     SRCNN_LAUNCH_TRY();
+    if (x6) {
+      const int totx = (N2 / 32) * (N1 / 16) * F2 * F2 * 512;
+      hipLaunchKernelGGL((wprep_w2x6_kernel<N1, N2, F2>), dim3((totx + 255) / 256), dim3(256), 0, s, W2, Wx);
+      SRCNN_LAUNCH_TRY();
+    }
   }
   {
     SRCNN_PROFILE("wide_l1_fwd", s);
@@ -1437,6 +1593,16 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
     SRCNN_LAUNCH_TRY();
   }
   {
+    SRCNN_PROFILE("wide_l2_fwd", s);
+    kernels_note(x6 ? "wl2x6_fwd" : "wide_l2_fwd");
+    if (x6) {
+      if (int rc = set_lds(wl2x6_fwd_kernel<N1, N2, F2, NetT::MT2>, lds6)) return rc;
+      hipLaunchKernelGGL((wl2x6_fwd_kernel<N1, N2, F2, NetT::MT2>), dim3(std::min(g.batch, GC)), dim3(256),
+                         lds6, s, A1, Wx, B2, A2, cf);
+      SRCNN_LAUNCH_TRY();
+    }
+  }
+  if (!x6) {
     SRCNN_PROFILE("wide_l2_fwd", s);
     const size_t lds = 2 * ((size_t)cf.img_w * cf.img_h * kPS + kImgSlack) * sizeof(float);
     if (int rc = set_lds(conv_mfma_kernel<N1, N2, F2, NetT::MT2, false>, lds)) return rc;
@@ -1688,8 +1854,9 @@ int preload(const srcnn_net* net) {
                      (const void*)wl3l_kernel<64, 5>, (const void*)wl3_kernel<64, 5>,
                      (const void*)d1g16_kernel<64, 128, 5, 9>,
                      (const void*)conv_mfma_kernel<64, 128, 5, NetT::MT4, true>,
-                     (const void*)prepack_w2_kernel<128, 64, 5>, (const void*)wgrad2_kernel<128, 64, 5>};
-  int rc = resolve_kernels(k, 9);
+                     (const void*)prepack_w2_kernel<128, 64, 5>, (const void*)wgrad2_kernel<128, 64, 5>,
+                     (const void*)wprep_w2x6_kernel<128, 64, 5>, (const void*)wl2x6_fwd_kernel<128, 64, 5, NetT::MT2>};
+  int rc = resolve_kernels(k, 11);
   return rc ? rc : 1;
 }
 

@@ -101,3 +101,38 @@ def test_split_forward_within_fp32_error(S, w, h):
     print("forward %dx%d: split %.3e  fp32 MFMA %.3e  fp32 oracle %.3e"
           % (w, h, errs[0], errs[1], normwise(ref32, ref64)))
     assert errs[0] <= 1.5 * errs[1] + 2.0 ** -24, errs
+
+
+WIDE = (128, 64, 9, 5, 5)
+
+
+@pytest.mark.parametrize("batch", [3, 16])
+def test_split_wide_l2_within_fp32_error(S, batch):
+    """The wide net's L2 forward (wl2x6_fwd vs conv_mfma): the whole gradient,
+    which every later layer computes from A2, segment by segment."""
+    rng = np.random.default_rng(5)
+    size = 33
+    X, T = make_batch(rng, batch, size, size)
+    params = make_params(rng, WIDE, sd=0.05)
+    P = params.size
+    g0 = np.zeros(P, np.float32)
+    g64, _ = orc.f64.train_fwd_bwd(WIDE, X, T, size, size, batch, params, g0)
+    res = {}
+    for arith in (0, 1):
+        S.set_arith(arith)
+        net = S.Net(*WIDE)
+        nbytes = S.train_workspace_bytes(net, size, size, batch)
+        ws = torch.empty(nbytes // 4 + 64, dtype=torch.float32, device="cuda")
+        g = D(g0)
+        err = torch.zeros(1, dtype=torch.float32, device="cuda")
+        S.train_fwd_bwd(net, D(X), D(T), size, size, batch, D(params), g, err, ws, nbytes)
+        res[arith] = (H(g), S.last_kernels())
+    assert "wl2x6_fwd" in res[0][1], res[0][1]
+    assert "wl2x6_fwd" not in res[1][1], res[1][1]
+    off = S.net_offsets(S.Net(*WIDE)) + [P]
+    for i, nm in enumerate(NAMES):
+        sl = slice(off[i], off[i + 1])
+        es, ef = normwise(res[0][0][sl], g64[sl]), normwise(res[1][0][sl], g64[sl])
+        log_record({"test": "split_wide", "batch": batch, "seg": nm, "err_split": es, "err_f32_mfma": ef})
+        print("wide %s batch %d: split %.3e  fp32 MFMA %.3e" % (nm, batch, es, ef))
+        assert es <= 1.5 * ef + 2.0 ** -24, (nm, es, ef)
