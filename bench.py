@@ -49,7 +49,8 @@ RIDGE = PEAK_FP32_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9)
 # 1024 FLOP/cycle/SIMD x 1024 SIMDs x 2.4 GHz) / 6
 PEAK_BF16_TFLOPS = 2516.6
 PEAK_SPLIT_TFLOPS = round(PEAK_BF16_TFLOPS / 6, 1)
-SPLIT_KERNELS = {"l12x6_fwd": "l12_fwd_mfma", "l12x6_fwd_lazy": "l12_fwd_mfma", "d1x6_grad12": "delta1_grad12_fused"}
+SPLIT_KERNELS = {"l12x6_fwd": "l12_fwd_mfma", "l12x6_fwd_lazy": "l12_fwd_mfma", "d1x6_grad12": "delta1_grad12_fused",
+                 "wl2x6_fwd": "wide_l2_fwd"}
 
 
 def split_profiled(S):
@@ -143,27 +144,34 @@ def fused_bytes(net, w, h):
     }
 
 
-def step_roof_ms(stats, n, work, tiles, net=DEFAULT_NET, w=TILE, h=TILE):
+def step_roof_ms(stats, n, work, tiles, net=DEFAULT_NET, w=TILE, h=TILE, split=()):
     """Fused-minimum step roofline (ms): sum over the kernels that ran of
     max(F / FP32 peak, B_min / HBM peak) with B_min from fused_bytes().  The
     small slab reduction / update launches (no stage work, ~1% of the step)
-    count as zero, so this is a lower bound of the step as built."""
+    count as zero, so this is a lower bound of the step as built.  Kernels
+    named in `split` are priced at the split-bf16 peak instead."""
     t = 0.0
     for name, (cnt, _) in stats.items():
         kw = kernel_work(name, work, net, w, h)
         if kw:
-            t += cnt / n * max(kw[0] * tiles / (cnt / n) / (PEAK_FP32_TFLOPS * 1e12),
+            peak = PEAK_SPLIT_TFLOPS if name in split else PEAK_FP32_TFLOPS
+            t += cnt / n * max(kw[0] * tiles / (cnt / n) / (peak * 1e12),
                                kw[1] * tiles / (cnt / n) / (PEAK_HBM_GBS * 1e9))
     return t * 1e3
 
 
-def step_roofline(fused_ms, layerwise_ms, ms):
+def step_roofline(fused_ms, layerwise_ms, ms, split_ms=None):
     """The step against its fused-minimum roof (t_roof_ms / frac: the bound of
     the kernels as fused) and, for reference, SURVEY.md 8(d)'s layer-by-layer
-    roof (each stage's tensors through HBM; the fused kernels can beat it)."""
-    return {"t_roof_ms": round(fused_ms, 4), "frac": round(fused_ms / ms, 4),
-            "model": "sum over the step's kernels of max(F/157.3 TF, B_min/8 TB/s)",
-            "layerwise_t_roof_ms": round(layerwise_ms, 4), "layerwise_frac": round(layerwise_ms / ms, 4)}
+    roof (each stage's tensors through HBM; the fused kernels can beat it).
+    split_ms: the same roof with the split-bf16 kernels at their own peak."""
+    out = {"t_roof_ms": round(fused_ms, 4), "frac": round(fused_ms / ms, 4),
+           "model": "sum over the step's kernels of max(F/157.3 TF, B_min/8 TB/s)",
+           "layerwise_t_roof_ms": round(layerwise_ms, 4), "layerwise_frac": round(layerwise_ms / ms, 4)}
+    if split_ms is not None:
+        out.update({"split_t_roof_ms": round(split_ms, 4), "split_frac": round(split_ms / ms, 4),
+                    "split_model": "as t_roof_ms, the split-bf16 kernels at %.1f TF" % PEAK_SPLIT_TFLOPS})
+    return out
 
 
 def kernel_work(name, work, net, w, h):
@@ -524,6 +532,7 @@ def wide_training(S, steps=5, warmup=2, batch=4096):
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     _mark("wide timed steps done")
+    split = split_profiled(S)
     S.profile_enable(False)
     stats = S.profile_stats()
     work = layer_work(net_t, w, h)
@@ -535,14 +544,16 @@ def wide_training(S, steps=5, warmup=2, batch=4096):
                for k, (c, t) in stats.items()}
     rooflines = {}
     for k, (c, t) in stats.items():
-        r = roofline_of(k, c / steps, t / steps, work, batch, load_pmc(), net_t, w, h)
+        r = roofline_of(k, c / steps, t / steps, work, batch, load_pmc(), net_t, w, h, split=k in split)
         if r:
             rooflines[k] = r
     return {"workload": "SRCNN wide n1=128 n2=64 f1=9 f2=5 f3=5, fp32 training, 33x33 tiles, "
                         "batch %d (BASELINE.json configs[3])" % batch,
             "tiles_s": round(batch * steps / el, 1), "ms_per_step": round(ms, 4), "steps": steps,
             "tflops": round(flops / (ms * 1e-3) / 1e12, 2),
-            "step_roofline": step_roofline(step_roof_ms(stats, steps, work, batch, net_t, w, h), t_roof * 1e3, ms),
+            "step_roofline": step_roofline(step_roof_ms(stats, steps, work, batch, net_t, w, h), t_roof * 1e3, ms,
+                                           step_roof_ms(stats, steps, work, batch, net_t, w, h, split)
+                                           if split else None),
             "kernel_path": S.last_path(), "kernels": kernels, "rooflines": rooflines}
 
 
@@ -1052,7 +1063,8 @@ def run(args, S, parallel, rank, world, local, device=None):
                                     else "env") if world > 1 else None},
             "roofline": roof,
             "rooflines": rooflines,
-            "step_roofline": step_roofline(step_roof_ms(stats, n_prof, work, B), t_roof * 1e3, ms_step),
+            "step_roofline": step_roofline(step_roof_ms(stats, n_prof, work, B), t_roof * 1e3, ms_step,
+                                           step_roof_ms(stats, n_prof, work, B, split=split) if split else None),
             "kernels": kernels,
             "profiled_steps": n_prof,
             "cpu_baseline": None,
