@@ -94,5 +94,19 @@ __device__ __forceinline__ f32x16 mma_x6(const bf16x8 (&a)[3], const bf16x8 (&b)
   return mma_bf16(a[0], b[0], c);
 }
 
+// the same on v_mfma_f32_16x16x32_bf16 (a 32-slot k-step, 16x16 C)
+__device__ __forceinline__ f32x4 mma16_bf16(const bf16x8& a, const bf16x8& b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ f32x4 mma16_x6(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x4 c) {
+  c = mma16_bf16(a[2], b[0], c);
+  c = mma16_bf16(a[1], b[1], c);
+  c = mma16_bf16(a[0], b[2], c);
+  c = mma16_bf16(a[1], b[0], c);
+  c = mma16_bf16(a[0], b[1], c);
+  return mma16_bf16(a[0], b[0], c);
+}
+
 }  // namespace mfma
 }  // namespace srcnn

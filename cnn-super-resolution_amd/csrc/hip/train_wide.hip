@@ -1470,6 +1470,223 @@ __global__ __launch_bounds__(512, 1) void wgrad2_kernel(const float* __restrict_
 }
 
 // ---------------------------------------------------------------------------
+// wgrad2x6: wgrad2 with split-bf16 products (split.hpp) on
+// v_mfma_f32_16x16x32_bf16: rows = 16 channels, cols = 16 n, K = 32 output
+// pixels per k-step as 4 RUNS of 8 consecutive pixels of an output row (lane
+// group gq = one run; a row of w2 <= 24 pixels is ceil(w2 / 8) runs, the
+// slots past w2 carry zero delta2).  Block = (16-channel slice cq, sample
+// group), 8 waves = (n half nh) x (tap group tg: taps 0-6 / 7-12 / 13-18 /
+// 19-24), a wave holding 2 n tiles x 7 taps of 16x16 accumulators (tap group
+// 3's spare slot sums gB2 with an all-ones A operand in the cq = 0 blocks).
+// Per sample, bands of 4 output rows (one k-step = the 4 rows' runs at one
+// column, so a read's 64 lanes hit 64 banks; a last band of < 4 rows packs
+// its runs row by row):
+//   A: A1 rows in a ring of 8, split, as PAIR images: dword x of (channel,
+//      part, ring row) holds the parts of pixels x and x + 1, so a run's 8
+//      values under any tap are dwords m, m+2, m+4, m+6 (two ds_read2_b32);
+//      ring rows 48 dwords apart, channels kG6CP (= 1 mod 64) apart
+//   B: the band's delta2 rows split, [part][row][n][24 px] bf16 (n pitch 12
+//      dwords: each 16-lane group of a ds_read_b128 conflict-free)
+// The next band's rows are register-staged (loads issued at the band's
+// start) and split into LDS after its MFMAs, between two barriers.
+// ---------------------------------------------------------------------------
+constexpr int kG6RowP = 48;                              // dwords per ring row (pair image)
+constexpr int kG6Ring = 8;                               // ring rows: a band of 4 + F - 1
+constexpr int kG6QP = kG6Ring * kG6RowP;                 // dwords per (channel, part)
+constexpr int kG6CP = 3 * kG6QP + 1;                     // dwords per channel (= 1 mod 64)
+constexpr int kG6A = 16 * kG6CP;                         // A ring dwords
+constexpr int kG6NP = 12;                                // dwords per delta2 (part, row, n): 24 px
+constexpr int kG6D = 3 * 4 * 64 * kG6NP;                 // delta2 image dwords
+constexpr size_t kG6Lds = (size_t)(kG6A + kG6D) * 4;     // 110.7 KB: one block per CU
+constexpr int kG6MaxW2 = 24, kG6Groups = 32;
+
+template <int CIN, int COUT, int F>
+__global__ __launch_bounds__(512, 1) void wgrad2x6_kernel(const float* __restrict__ A1,
+                                                         const float* __restrict__ D2,
+                                                         float* __restrict__ slab2, G2Geom g) {
+  using mfma::bf16x8;
+  using mfma::u32x4;
+  constexpr int FF = F * F, NCQ = CIN / 16, TG = (FF + 3) / 4;
+  static_assert(CIN % 16 == 0 && COUT == 64 && F <= 5 && FF % 4 == 1, "shape");
+  constexpr size_t P2 = (size_t)FF * CIN * COUT + COUT;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  uint32_t* const ra = reinterpret_cast<uint32_t*>(smem);
+  uint16_t* const rah = reinterpret_cast<uint16_t*>(smem);
+  uint16_t* const dh = reinterpret_cast<uint16_t*>(smem + kG6A);
+  const int lane = lane_id(), wave = wave_id(), i16 = lane & 15, gq = lane >> 4;
+  const int nh = wave & 1, tg = wave >> 1;
+  const int t0 = tg == 0 ? 0 : TG + (tg - 1) * (TG - 1), tcnt = tg == 0 ? TG : TG - 1;
+  int cq = blockIdx.x % NCQ, grp = blockIdx.x / NCQ;
+  if (gridDim.x % (8 * NCQ) == 0) {  // a group's NCQ slices on one XCD (wgrad2)
+    const int j = blockIdx.x / 8;
+    cq = j % NCQ;
+    grp = blockIdx.x % 8 + 8 * (j / NCQ);
+  }
+  const bool gbw = cq == 0 && tg == 3;  // (tap group 3 has TG - 1 taps: slot TG - 1 is free)
+  const int w1 = g.w1, h1 = g.h1, w2 = g.w2, h2 = g.h2;
+  const int nb = (h2 + 3) / 4, nrx = (w2 + 7) / 8;
+  for (int e = threadIdx.x; e < kG6A + kG6D; e += 512) ra[e] = 0u;
+  f32x4 acc[TG][2];
+#pragma unroll
+  for (int t = 0; t < TG; t++) acc[t][0] = acc[t][1] = zero4();
+  const int nsamp = g.batch > grp ? (g.batch - grp + g.groups - 1) / g.groups : 0;
+  const int nunits = nsamp * nb;
+  // register staging: up to 8 A1 rows x w1 pixels x 4 channel quads, and 4
+  // delta2 rows x w2 pixels x 16 n quads (pixel fastest: the LDS writes of
+  // adjacent lanes are adjacent)
+  constexpr int kAQ = (kG6Ring * (kG6MaxW2 + F - 1) * 4 + 511) / 512;
+  constexpr int kDQ = (4 * kG6MaxW2 * 16 + 511) / 512;
+  f32x4 xa[kAQ], xd[kDQ];
+  auto rows_of = [&](int u, int& s, int& b, int& alo, int& ahi) __attribute__((always_inline)) {
+    s = grp + (u / nb) * g.groups;
+    b = u % nb;
+    alo = b == 0 ? 0 : 4 * b + 4;
+    ahi = min(4 * b + 8, h1);
+  };
+  auto load = [&](int u) __attribute__((always_inline)) {
+    int s, b, alo, ahi;
+    rows_of(u, s, b, alo, ahi);
+    const int na = (ahi - alo) * w1 * 4;
+    // (every load is issued, the unused ones at offset 0: a conditional load
+    // into a register makes the compiler wait for each load before the next)
+#pragma unroll
+    for (int k = 0; k < kAQ; k++) {
+      const int i = threadIdx.x + 512 * k, px = i % w1, rest = i / w1, qq = rest & 3, r = rest >> 2;
+      const size_t o = (((size_t)s * h1 + alo + r) * w1 + px) * CIN + 16 * cq + 4 * qq;
+      xa[k] = *reinterpret_cast<const f32x4*>(A1 + (i < na ? o : 0));
+    }
+#pragma unroll
+    for (int k = 0; k < kDQ; k++) {
+      const int i = threadIdx.x + 512 * k, px = i % w2, rest = i / w2, r = rest & 3, nq = rest >> 2;
+      const int row = 4 * b + r;
+      const bool ok = i < 64 * w2 && row < h2;
+      const size_t o = (((size_t)s * h2 + row) * w2 + px) * COUT + 4 * nq;
+      xd[k] = *reinterpret_cast<const f32x4*>(D2 + (ok ? o : 0));
+    }
+  };
+  auto store = [&](int u) __attribute__((always_inline)) {
+    int s, b, alo, ahi;
+    rows_of(u, s, b, alo, ahi);
+    const int na = (ahi - alo) * w1 * 4;
+#pragma unroll
+    for (int k = 0; k < kAQ; k++) {
+      const int i = threadIdx.x + 512 * k, px = i % w1, rest = i / w1, qq = rest & 3, r = rest >> 2;
+      if (i < na) {
+        const int slot = (alo + r) & (kG6Ring - 1);
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+          __bf16 p[3];
+          mfma::split3(xa[k][e], p[0], p[1], p[2]);
+          const int d = (4 * qq + e) * kG6CP + slot * kG6RowP + px;
+#pragma unroll
+          for (int q = 0; q < 3; q++) {
+            const uint16_t v = __builtin_bit_cast(uint16_t, p[q]);
+            rah[2 * (d + q * kG6QP)] = v;                  // pair dword px, low half
+            if (px > 0) rah[2 * (d + q * kG6QP) - 1] = v;  // pair dword px - 1, high half
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kDQ; k++) {
+      const int i = threadIdx.x + 512 * k, px = i % w2, rest = i / w2, r = rest & 3, nq = rest >> 2;
+      if (i < 64 * w2) {
+        const bool ok = 4 * b + r < h2;  // rows past the image: zero delta2
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+          __bf16 p[3];
+          mfma::split3(ok ? xd[k][e] : 0.0f, p[0], p[1], p[2]);
+#pragma unroll
+          for (int q = 0; q < 3; q++)
+            dh[((q * 4 + r) * 64 + 4 * nq + e) * (2 * kG6NP) + px] = __builtin_bit_cast(uint16_t, p[q]);
+        }
+      }
+    }
+  };
+  if (nunits > 0) {
+    load(0);
+    __syncthreads();  // (the LDS clear)
+    store(0);
+  }
+  __syncthreads();
+  bf16x8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; e++) ones[e] = (__bf16)1.0f;
+  for (int u = 0; u < nunits; u++) {
+    if (u + 1 < nunits) load(u + 1);
+    const int y0 = 4 * (u % nb), nr = min(4, h2 - y0);
+    const bool full = nr == 4;
+    const int nks = full ? nrx : (nr * nrx + 3) / 4;
+    for (int kk = 0; kk < nks; kk++) {
+      // this lane group's run: band row rg, first column x0
+      const int j = 4 * kk + gq, rg = full ? gq : j / nrx, x0 = full ? 8 * kk : 8 * (j - rg * nrx);
+      bf16x8 bq[2][3];
+#pragma unroll
+      for (int n2 = 0; n2 < 2; n2++)
+#pragma unroll
+        for (int q = 0; q < 3; q++)
+          bq[n2][q] = *reinterpret_cast<const bf16x8*>(
+              dh + ((q * 4 + rg) * 64 + 32 * nh + 16 * n2 + i16) * (2 * kG6NP) + x0);
+      const int ab = i16 * kG6CP + x0, yr = y0 + rg;
+      // tap slot ti's A operand (slot TG - 1 of tap groups 1-3 reads a valid
+      // address and is not used)
+      auto rda = [&](int ti, bf16x8 (&a)[3]) __attribute__((always_inline)) {
+        const int t = min(t0 + ti, FF - 1), dy = t / F, dx = t - dy * F;
+        const uint32_t* pa = ra + ab + ((yr + dy) & (kG6Ring - 1)) * kG6RowP + dx;
+#pragma unroll
+        for (int q = 0; q < 3; q++) {
+          u32x4 w;
+          w[0] = pa[q * kG6QP];
+          w[1] = pa[q * kG6QP + 2];
+          w[2] = pa[q * kG6QP + 4];
+          w[3] = pa[q * kG6QP + 6];
+          a[q] = __builtin_bit_cast(bf16x8, w);
+        }
+      };
+      // slots 0 .. TG - 2 (every wave's) without branches, each slot's reads
+      // issued under the previous slot's MFMAs; then the last slot
+      bf16x8 a2[2][3];
+      rda(0, a2[0]);
+#pragma unroll
+      for (int ti = 0; ti < TG - 1; ti++) {
+        rda(ti + 1, a2[(ti + 1) & 1]);
+        acc[ti][0] = mfma::mma16_x6(a2[ti & 1], bq[0], acc[ti][0]);
+        acc[ti][1] = mfma::mma16_x6(a2[ti & 1], bq[1], acc[ti][1]);
+      }
+      if (tcnt == TG) {
+        acc[TG - 1][0] = mfma::mma16_x6(a2[(TG - 1) & 1], bq[0], acc[TG - 1][0]);
+        acc[TG - 1][1] = mfma::mma16_x6(a2[(TG - 1) & 1], bq[1], acc[TG - 1][1]);
+      } else if (gbw) {
+        // gB2[n] += sum_k delta2[k][n]: the three parts against ones
+#pragma unroll
+        for (int n2 = 0; n2 < 2; n2++)
+#pragma unroll
+          for (int q = 0; q < 3; q++) acc[TG - 1][n2] = mfma::mma16_bf16(ones, bq[n2][q], acc[TG - 1][n2]);
+      }
+    }
+    __syncthreads();  // the band's operands are consumed
+    if (u + 1 < nunits) store(u + 1);
+    __syncthreads();
+  }
+  // slab rows of this block: channels 16 cq + 4 gq + r, n = 32 nh + 16 n2 + i16
+  float* out = slab2 + (size_t)grp * P2;
+#pragma unroll
+  for (int ti = 0; ti < TG; ti++) {
+    if (ti < tcnt) {
+      const int t = t0 + ti;
+#pragma unroll
+      for (int n2 = 0; n2 < 2; n2++)
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+          out[((size_t)t * CIN + 16 * cq + 4 * gq + r) * COUT + 32 * nh + 16 * n2 + i16] = acc[ti][n2][r];
+    } else if (gbw && gq == 0) {
+#pragma unroll
+      for (int n2 = 0; n2 < 2; n2++) out[(size_t)FF * CIN * COUT + 32 * nh + 16 * n2 + i16] = acc[ti][n2][0];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
 template <int N1, int N2, int F1, int F2, int F3>
@@ -1553,6 +1770,9 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   const size_t lds6 = 2 * (size_t)cf.img_w * cf.img_h * kW6Row * sizeof(float);
   const bool x6 = g_arith == 0 && N2 == 64 && N1 % 16 == 0 && cf.img_w * cf.img_h <= kW6ImgMax;
   const size_t n1 = align_f((size_t)G1 * NetT::P1), n2 = align_f((size_t)g2.groups * NetT::P2);
+  // the split-bf16 wgrad2 (wgrad2x6): fewer sample groups (one block per CU), so the slab fits
+  const bool x6g = g_arith == 0 && F2 == 5 && N2 == 64 && N1 % 16 == 0 && g.w2 <= kG6MaxW2;
+  if (x6g) g2.groups = (int)std::min<uint32_t>(batch, kG6Groups);
   const size_t n3 = align_f((size_t)G3 * NetT::P3), nsq = align_f(G3);
   const size_t bytes = (nWf + nWd + nWx + n1 + n2 + n3 + nsq) * sizeof(float);
   if (query_only) {
@@ -1633,6 +1853,16 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
     SRCNN_LAUNCH_TRY();
   }
   {
+    SRCNN_PROFILE("wide_grad2", s);
+    kernels_note(x6g ? "wgrad2x6" : "wgrad2");
+    if (x6g) {
+      if (int rc = set_lds(wgrad2x6_kernel<N1, N2, F2>, kG6Lds)) return rc;
+      hipLaunchKernelGGL((wgrad2x6_kernel<N1, N2, F2>), dim3(g2.groups * (N1 / 16)), dim3(512), kG6Lds, s, A1,
+                         D2, slab2, g2);
+      SRCNN_LAUNCH_TRY();
+    }
+  }
+  if (!x6g) {
     SRCNN_PROFILE("wide_grad2", s);
     const size_t lds = 2 * (size_t)kGBuf * sizeof(float);
     if (int rc = set_lds(wgrad2_kernel<N1, N2, F2>, lds)) return rc;
@@ -1855,8 +2085,9 @@ int preload(const srcnn_net* net) {
                      (const void*)d1g16_kernel<64, 128, 5, 9>,
                      (const void*)conv_mfma_kernel<64, 128, 5, NetT::MT4, true>,
                      (const void*)prepack_w2_kernel<128, 64, 5>, (const void*)wgrad2_kernel<128, 64, 5>,
-                     (const void*)wprep_w2x6_kernel<128, 64, 5>, (const void*)wl2x6_fwd_kernel<128, 64, 5, NetT::MT2>};
-  int rc = resolve_kernels(k, 11);
+                     (const void*)wprep_w2x6_kernel<128, 64, 5>, (const void*)wl2x6_fwd_kernel<128, 64, 5, NetT::MT2>,
+                     (const void*)wgrad2x6_kernel<128, 64, 5>};
+  int rc = resolve_kernels(k, 12);
   return rc ? rc : 1;
 }
 

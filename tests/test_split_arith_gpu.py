@@ -106,17 +106,17 @@ def test_split_forward_within_fp32_error(S, w, h):
 WIDE = (128, 64, 9, 5, 5)
 
 
-@pytest.mark.parametrize("batch", [3, 16])
-def test_split_wide_l2_within_fp32_error(S, batch):
-    """The wide net's L2 forward (wl2x6_fwd vs conv_mfma): the whole gradient,
-    which every later layer computes from A2, segment by segment."""
+@pytest.mark.parametrize("batch,size", [(3, 33), (16, 33), (5, 29), (4, 25), (3, 27)])
+def test_split_wide_within_fp32_error(S, batch, size):
+    """The wide net's split kernels (wl2x6_fwd, wgrad2x6 against conv_mfma,
+    wgrad2): the whole gradient, segment by segment."""
     rng = np.random.default_rng(5)
-    size = 33
     X, T = make_batch(rng, batch, size, size)
     params = make_params(rng, WIDE, sd=0.05)
     P = params.size
     g0 = np.zeros(P, np.float32)
     g64, _ = orc.f64.train_fwd_bwd(WIDE, X, T, size, size, batch, params, g0)
+    g32, _ = orc.train_fwd_bwd(WIDE, X, T, size, size, batch, params, g0)
     res = {}
     for arith in (0, 1):
         S.set_arith(arith)
@@ -127,12 +127,17 @@ def test_split_wide_l2_within_fp32_error(S, batch):
         err = torch.zeros(1, dtype=torch.float32, device="cuda")
         S.train_fwd_bwd(net, D(X), D(T), size, size, batch, D(params), g, err, ws, nbytes)
         res[arith] = (H(g), S.last_kernels())
-    assert "wl2x6_fwd" in res[0][1], res[0][1]
-    assert "wl2x6_fwd" not in res[1][1], res[1][1]
+    assert "wl2x6_fwd" in res[0][1] and "wgrad2x6" in res[0][1], res[0][1]
+    assert "x6" not in res[1][1], res[1][1]
     off = S.net_offsets(S.Net(*WIDE)) + [P]
     for i, nm in enumerate(NAMES):
         sl = slice(off[i], off[i + 1])
         es, ef = normwise(res[0][0][sl], g64[sl]), normwise(res[1][0][sl], g64[sl])
-        log_record({"test": "split_wide", "batch": batch, "seg": nm, "err_split": es, "err_f32_mfma": ef})
-        print("wide %s batch %d: split %.3e  fp32 MFMA %.3e" % (nm, batch, es, ef))
-        assert es <= 1.5 * ef + 2.0 ** -24, (nm, es, ef)
+        eo = normwise(g32[sl], g64[sl])
+        log_record({"test": "split_wide", "batch": batch, "size": size, "seg": nm, "err_split": es,
+                    "err_f32_mfma": ef, "err_f32_oracle": eo})
+        print("wide %s batch %d size %d: split %.3e  fp32 MFMA %.3e  fp32 oracle %.3e" % (nm, batch, size, es, ef, eo))
+        # (B3 is one sum over every delta3 with heavy cancellation: either fp32
+        # computation can land far closer to the fp64 value by chance, so the
+        # bound is the larger of the two fp32 errors)
+        assert es <= 1.5 * max(ef, eo) + 2.0 ** -24, (nm, es, ef, eo)
