@@ -1531,12 +1531,18 @@ __global__ __launch_bounds__(512, 1) void wgrad2x6_kernel(const float* __restric
   for (int t = 0; t < TG; t++) acc[t][0] = acc[t][1] = zero4();
   const int nsamp = g.batch > grp ? (g.batch - grp + g.groups - 1) / g.groups : 0;
   const int nunits = nsamp * nb;
-  // register staging: up to 8 A1 rows x w1 pixels x 4 channel quads, and 4
-  // delta2 rows x w2 pixels x 16 n quads (pixel fastest: the LDS writes of
-  // adjacent lanes are adjacent)
-  constexpr int kAQ = (kG6Ring * (kG6MaxW2 + F - 1) * 4 + 511) / 512;
-  constexpr int kDQ = (4 * kG6MaxW2 * 16 + 511) / 512;
-  f32x4 xa[kAQ], xd[kDQ];
+  // register staging in runs of 8 pixels (coalesced loads, 16-B LDS writes):
+  //   delta2: threads 0-191 = (band row r, run xr, n quad nq), 8 pixels x 4 n
+  //   A1:     threads 256-383 = (ring row r, run xr, channel quad qq), the
+  //           run's 8 pixels + the next one (the pair image's last dword)
+  // Every thread issues every load (idle ones at offset 0, one address per
+  // instruction): a conditional load into a register makes the compiler wait
+  // for each load before issuing the next.
+  const int tid = threadIdx.x;
+  const bool drole = tid < 192, arole = tid >= 256 && tid < 384;
+  const int dnq = tid & 15, dru = (tid >> 4) % 12, dr = dru / 3, dxr = dru - 3 * dr;
+  const int ta = (tid - 256) & 127, aqq = ta & 3, aru = ta >> 2, ar = aru >> 2, axr = aru & 3;
+  f32x4 xa[9], xd[8];
   auto rows_of = [&](int u, int& s, int& b, int& alo, int& ahi) __attribute__((always_inline)) {
     s = grp + (u / nb) * g.groups;
     b = u % nb;
@@ -1546,60 +1552,59 @@ __global__ __launch_bounds__(512, 1) void wgrad2x6_kernel(const float* __restric
   auto load = [&](int u) __attribute__((always_inline)) {
     int s, b, alo, ahi;
     rows_of(u, s, b, alo, ahi);
-    const int na = (ahi - alo) * w1 * 4;
-    // (every load is issued, the unused ones at offset 0: a conditional load
-    // into a register makes the compiler wait for each load before the next)
+    const bool aok = arole && alo + ar < ahi;
+    const size_t abase = (((size_t)s * h1 + alo + ar) * w1 + 8 * axr) * CIN + 16 * cq + 4 * aqq;
 #pragma unroll
-    for (int k = 0; k < kAQ; k++) {
-      const int i = threadIdx.x + 512 * k, px = i % w1, rest = i / w1, qq = rest & 3, r = rest >> 2;
-      const size_t o = (((size_t)s * h1 + alo + r) * w1 + px) * CIN + 16 * cq + 4 * qq;
-      xa[k] = *reinterpret_cast<const f32x4*>(A1 + (i < na ? o : 0));
-    }
+    for (int j = 0; j < 9; j++)
+      xa[j] = *reinterpret_cast<const f32x4*>(A1 + (aok && 8 * axr + j < w1 ? abase + (size_t)j * CIN : 0));
+    const int row = 4 * b + dr;
+    const bool dok = drole && dxr < nrx && row < h2;
+    const size_t dbase = (((size_t)s * h2 + row) * w2 + 8 * dxr) * COUT + 4 * dnq;
 #pragma unroll
-    for (int k = 0; k < kDQ; k++) {
-      const int i = threadIdx.x + 512 * k, px = i % w2, rest = i / w2, r = rest & 3, nq = rest >> 2;
-      const int row = 4 * b + r;
-      const bool ok = i < 64 * w2 && row < h2;
-      const size_t o = (((size_t)s * h2 + row) * w2 + px) * COUT + 4 * nq;
-      xd[k] = *reinterpret_cast<const f32x4*>(D2 + (ok ? o : 0));
-    }
+    for (int j = 0; j < 8; j++)
+      xd[j] = *reinterpret_cast<const f32x4*>(D2 + (dok && 8 * dxr + j < w2 ? dbase + (size_t)j * COUT : 0));
   };
   auto store = [&](int u) __attribute__((always_inline)) {
     int s, b, alo, ahi;
     rows_of(u, s, b, alo, ahi);
-    const int na = (ahi - alo) * w1 * 4;
+    if (arole && alo + ar < ahi) {
+      const int slot = (alo + ar) & (kG6Ring - 1);
 #pragma unroll
-    for (int k = 0; k < kAQ; k++) {
-      const int i = threadIdx.x + 512 * k, px = i % w1, rest = i / w1, qq = rest & 3, r = rest >> 2;
-      if (i < na) {
-        const int slot = (alo + r) & (kG6Ring - 1);
+      for (int e = 0; e < 4; e++) {
+        float v[8];
 #pragma unroll
-        for (int e = 0; e < 4; e++) {
-          __bf16 p[3];
-          mfma::split3(xa[k][e], p[0], p[1], p[2]);
-          const int d = (4 * qq + e) * kG6CP + slot * kG6RowP + px;
+        for (int j = 0; j < 8; j++) v[j] = 8 * axr + j < w1 ? xa[j][e] : 0.0f;
+        bf16x8 pp[3];
+        mfma::split8(v, pp);
+        __bf16 p8[3];
+        mfma::split3(8 * axr + 8 < w1 ? xa[8][e] : 0.0f, p8[0], p8[1], p8[2]);
+        uint32_t* d = ra + (4 * aqq + e) * kG6CP + slot * kG6RowP + 8 * axr;
 #pragma unroll
-          for (int q = 0; q < 3; q++) {
-            const uint16_t v = __builtin_bit_cast(uint16_t, p[q]);
-            rah[2 * (d + q * kG6QP)] = v;                  // pair dword px, low half
-            if (px > 0) rah[2 * (d + q * kG6QP) - 1] = v;  // pair dword px - 1, high half
-          }
+        for (int q = 0; q < 3; q++) {
+          const u32x4 lo = __builtin_bit_cast(u32x4, pp[q]);  // parts of pixels 2i, 2i + 1 (i < 4)
+          uint32_t w[8];
+#pragma unroll
+          for (int i = 0; i < 4; i++) w[2 * i] = lo[i];
+#pragma unroll
+          for (int i = 0; i < 3; i++) w[2 * i + 1] = (lo[i] >> 16) | (lo[i + 1] << 16);
+          w[7] = (lo[3] >> 16) | ((uint32_t)__builtin_bit_cast(uint16_t, p8[q]) << 16);
+#pragma unroll
+          for (int i = 0; i < 8; i++) d[q * kG6QP + i] = w[i];
         }
       }
     }
+    if (drole && dxr < nrx) {
+      const bool rok = 4 * b + dr < h2;  // rows past the image: zero delta2
 #pragma unroll
-    for (int k = 0; k < kDQ; k++) {
-      const int i = threadIdx.x + 512 * k, px = i % w2, rest = i / w2, r = rest & 3, nq = rest >> 2;
-      if (i < 64 * w2) {
-        const bool ok = 4 * b + r < h2;  // rows past the image: zero delta2
+      for (int e = 0; e < 4; e++) {
+        float v[8];
 #pragma unroll
-        for (int e = 0; e < 4; e++) {
-          __bf16 p[3];
-          mfma::split3(ok ? xd[k][e] : 0.0f, p[0], p[1], p[2]);
+        for (int j = 0; j < 8; j++) v[j] = rok && 8 * dxr + j < w2 ? xd[j][e] : 0.0f;
+        bf16x8 pp[3];
+        mfma::split8(v, pp);
 #pragma unroll
-          for (int q = 0; q < 3; q++)
-            dh[((q * 4 + r) * 64 + 4 * nq + e) * (2 * kG6NP) + px] = __builtin_bit_cast(uint16_t, p[q]);
-        }
+        for (int q = 0; q < 3; q++)
+          *reinterpret_cast<bf16x8*>(dh + ((q * 4 + dr) * 64 + 4 * dnq + e) * (2 * kG6NP) + 8 * dxr) = pp[q];
       }
     }
   };
@@ -1616,7 +1621,11 @@ __global__ __launch_bounds__(512, 1) void wgrad2x6_kernel(const float* __restric
     if (u + 1 < nunits) load(u + 1);
     const int y0 = 4 * (u % nb), nr = min(4, h2 - y0);
     const bool full = nr == 4;
+#if SRCNN_WG6_DIAG == 2  // timing diagnostic (results invalid): no k-steps
+    const int nks = 0;
+#else
     const int nks = full ? nrx : (nr * nrx + 3) / 4;
+#endif
     for (int kk = 0; kk < nks; kk++) {
       // this lane group's run: band row rg, first column x0
       const int j = 4 * kk + gq, rg = full ? gq : j / nrx, x0 = full ? 8 * kk : 8 * (j - rg * nrx);
@@ -1665,7 +1674,11 @@ __global__ __launch_bounds__(512, 1) void wgrad2x6_kernel(const float* __restric
       }
     }
     __syncthreads();  // the band's operands are consumed
+#if SRCNN_WG6_DIAG == 1  // timing diagnostic (results invalid): no staging stores
+    if (u + 1 < nunits && xa[0][0] == 1.2345f && xd[0][0] == 1.2345f) store(u + 1);
+#else
     if (u + 1 < nunits) store(u + 1);
+#endif
     __syncthreads();
   }
   // slab rows of this block: channels 16 cq + 4 gq + r, n = 32 nh + 16 n2 + i16
