@@ -1505,6 +1505,7 @@ __global__ __launch_bounds__(512, 1) void wgrad2x6_kernel(const float* __restric
                                                          const float* __restrict__ D2,
                                                          float* __restrict__ slab2, G2Geom g) {
   using mfma::bf16x8;
+  using mfma::f32x2;
   using mfma::u32x4;
   constexpr int FF = F * F, NCQ = CIN / 16, TG = (FF + 3) / 4;
   static_assert(CIN % 16 == 0 && COUT == 64 && F <= 5 && FF % 4 == 1, "shape");
@@ -1531,18 +1532,20 @@ __global__ __launch_bounds__(512, 1) void wgrad2x6_kernel(const float* __restric
   for (int t = 0; t < TG; t++) acc[t][0] = acc[t][1] = zero4();
   const int nsamp = g.batch > grp ? (g.batch - grp + g.groups - 1) / g.groups : 0;
   const int nunits = nsamp * nb;
-  // register staging in runs of 8 pixels (coalesced loads, 16-B LDS writes):
-  //   delta2: threads 0-191 = (band row r, run xr, n quad nq), 8 pixels x 4 n
-  //   A1:     threads 256-383 = (ring row r, run xr, channel quad qq), the
-  //           run's 8 pixels + the next one (the pair image's last dword)
-  // Every thread issues every load (idle ones at offset 0, one address per
-  // instruction): a conditional load into a register makes the compiler wait
-  // for each load before issuing the next.
+  // register staging in runs of 8 pixels (coalesced loads, 16-B LDS writes),
+  // by wave role:
+  //   waves 0-5, delta2: thread = (band row dr, run dxr, n pair dnp), the
+  //     run's 8 pixels x 2 n (a wave's load: two pixels' 64 n, 512 B)
+  //   waves 6-7, A1: thread = (ring row, run axr, channel pair acp), the
+  //     run's 8 pixels + the next one (the pair image's last dword) x 2
+  //     channels; two passes for a band's first 8 rows
+  // Each role's loads sit in one wave-uniform branch (loads in per-load
+  // branches make the compiler wait for each before issuing the next).
   const int tid = threadIdx.x;
-  const bool drole = tid < 192, arole = tid >= 256 && tid < 384;
-  const int dnq = tid & 15, dru = (tid >> 4) % 12, dr = dru / 3, dxr = dru - 3 * dr;
-  const int ta = (tid - 256) & 127, aqq = ta & 3, aru = ta >> 2, ar = aru >> 2, axr = aru & 3;
-  f32x4 xa[9], xd[8];
+  const bool drole = wave < 6;
+  const int dnp = tid & 31, dru = (tid >> 5) % 12, dr = dru / 3, dxr = dru - 3 * dr;
+  const int ta = tid & 127, acp = ta & 7, aru = ta >> 3, ar = aru >> 2, axr = aru & 3;
+  f32x2 xa[2][9], xd[8];
   auto rows_of = [&](int u, int& s, int& b, int& alo, int& ahi) __attribute__((always_inline)) {
     s = grp + (u / nb) * g.groups;
     b = u % nb;
@@ -1552,51 +1555,63 @@ __global__ __launch_bounds__(512, 1) void wgrad2x6_kernel(const float* __restric
   auto load = [&](int u) __attribute__((always_inline)) {
     int s, b, alo, ahi;
     rows_of(u, s, b, alo, ahi);
-    const bool aok = arole && alo + ar < ahi;
-    const size_t abase = (((size_t)s * h1 + alo + ar) * w1 + 8 * axr) * CIN + 16 * cq + 4 * aqq;
+    if (drole) {
+      const int row = 4 * b + dr;
+      const bool dok = dxr < nrx && row < h2;
+      const size_t dbase = (((size_t)s * h2 + row) * w2 + 8 * dxr) * COUT + 2 * dnp;
 #pragma unroll
-    for (int j = 0; j < 9; j++)
-      xa[j] = *reinterpret_cast<const f32x4*>(A1 + (aok && 8 * axr + j < w1 ? abase + (size_t)j * CIN : 0));
-    const int row = 4 * b + dr;
-    const bool dok = drole && dxr < nrx && row < h2;
-    const size_t dbase = (((size_t)s * h2 + row) * w2 + 8 * dxr) * COUT + 4 * dnq;
+      for (int j = 0; j < 8; j++)
+        xd[j] = *reinterpret_cast<const f32x2*>(D2 + (dok && 8 * dxr + j < w2 ? dbase + (size_t)j * COUT : 0));
+    } else {
 #pragma unroll
-    for (int j = 0; j < 8; j++)
-      xd[j] = *reinterpret_cast<const f32x4*>(D2 + (dok && 8 * dxr + j < w2 ? dbase + (size_t)j * COUT : 0));
+      for (int pass = 0; pass < 2; pass++) {
+        const int row = alo + ar + 4 * pass;
+        const size_t abase = (((size_t)s * h1 + row) * w1 + 8 * axr) * CIN + 16 * cq + 2 * acp;
+#pragma unroll
+        for (int j = 0; j < 9; j++)
+          xa[pass][j] = *reinterpret_cast<const f32x2*>(
+              A1 + (row < ahi && 8 * axr + j < w1 ? abase + (size_t)j * CIN : 0));
+      }
+    }
   };
   auto store = [&](int u) __attribute__((always_inline)) {
     int s, b, alo, ahi;
     rows_of(u, s, b, alo, ahi);
-    if (arole && alo + ar < ahi) {
-      const int slot = (alo + ar) & (kG6Ring - 1);
+    if (!drole) {
 #pragma unroll
-      for (int e = 0; e < 4; e++) {
-        float v[8];
+      for (int pass = 0; pass < 2; pass++) {
+        const int row = alo + ar + 4 * pass;
+        if (row < ahi) {
+          const int slot = row & (kG6Ring - 1);
 #pragma unroll
-        for (int j = 0; j < 8; j++) v[j] = 8 * axr + j < w1 ? xa[j][e] : 0.0f;
-        bf16x8 pp[3];
-        mfma::split8(v, pp);
-        __bf16 p8[3];
-        mfma::split3(8 * axr + 8 < w1 ? xa[8][e] : 0.0f, p8[0], p8[1], p8[2]);
-        uint32_t* d = ra + (4 * aqq + e) * kG6CP + slot * kG6RowP + 8 * axr;
+          for (int e = 0; e < 2; e++) {
+            float v[8];
 #pragma unroll
-        for (int q = 0; q < 3; q++) {
-          const u32x4 lo = __builtin_bit_cast(u32x4, pp[q]);  // parts of pixels 2i, 2i + 1 (i < 4)
-          uint32_t w[8];
+            for (int j = 0; j < 8; j++) v[j] = 8 * axr + j < w1 ? xa[pass][j][e] : 0.0f;
+            bf16x8 pp[3];
+            mfma::split8(v, pp);
+            __bf16 p8[3];
+            mfma::split3(8 * axr + 8 < w1 ? xa[pass][8][e] : 0.0f, p8[0], p8[1], p8[2]);
+            uint32_t* d = ra + (2 * acp + e) * kG6CP + slot * kG6RowP + 8 * axr;
 #pragma unroll
-          for (int i = 0; i < 4; i++) w[2 * i] = lo[i];
+            for (int q = 0; q < 3; q++) {
+              const u32x4 lo = __builtin_bit_cast(u32x4, pp[q]);  // parts of pixels 2i, 2i + 1 (i < 4)
+              uint32_t w[8];
 #pragma unroll
-          for (int i = 0; i < 3; i++) w[2 * i + 1] = (lo[i] >> 16) | (lo[i + 1] << 16);
-          w[7] = (lo[3] >> 16) | ((uint32_t)__builtin_bit_cast(uint16_t, p8[q]) << 16);
+              for (int i = 0; i < 4; i++) w[2 * i] = lo[i];
 #pragma unroll
-          for (int i = 0; i < 8; i++) d[q * kG6QP + i] = w[i];
+              for (int i = 0; i < 3; i++) w[2 * i + 1] = (lo[i] >> 16) | (lo[i + 1] << 16);
+              w[7] = (lo[3] >> 16) | ((uint32_t)__builtin_bit_cast(uint16_t, p8[q]) << 16);
+#pragma unroll
+              for (int i = 0; i < 8; i++) d[q * kG6QP + i] = w[i];
+            }
+          }
         }
       }
-    }
-    if (drole && dxr < nrx) {
+    } else if (dxr < nrx) {
       const bool rok = 4 * b + dr < h2;  // rows past the image: zero delta2
 #pragma unroll
-      for (int e = 0; e < 4; e++) {
+      for (int e = 0; e < 2; e++) {
         float v[8];
 #pragma unroll
         for (int j = 0; j < 8; j++) v[j] = rok && 8 * dxr + j < w2 ? xd[j][e] : 0.0f;
@@ -1604,7 +1619,7 @@ __global__ __launch_bounds__(512, 1) void wgrad2x6_kernel(const float* __restric
         mfma::split8(v, pp);
 #pragma unroll
         for (int q = 0; q < 3; q++)
-          *reinterpret_cast<bf16x8*>(dh + ((q * 4 + dr) * 64 + 4 * dnq + e) * (2 * kG6NP) + 8 * dxr) = pp[q];
+          *reinterpret_cast<bf16x8*>(dh + ((q * 4 + dr) * 64 + 2 * dnp + e) * (2 * kG6NP) + 8 * dxr) = pp[q];
       }
     }
   };
@@ -1618,7 +1633,9 @@ __global__ __launch_bounds__(512, 1) void wgrad2x6_kernel(const float* __restric
 #pragma unroll
   for (int e = 0; e < 8; e++) ones[e] = (__bf16)1.0f;
   for (int u = 0; u < nunits; u++) {
+#if SRCNN_WG6_DIAG != 3  // (3: timing diagnostic, results invalid: no staging loads)
     if (u + 1 < nunits) load(u + 1);
+#endif
     const int y0 = 4 * (u % nb), nr = min(4, h2 - y0);
     const bool full = nr == 4;
 #if SRCNN_WG6_DIAG == 2  // timing diagnostic (results invalid): no k-steps
