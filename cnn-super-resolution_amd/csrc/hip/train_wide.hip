@@ -1633,16 +1633,10 @@ __global__ __launch_bounds__(512, 1) void wgrad2x6_kernel(const float* __restric
 #pragma unroll
   for (int e = 0; e < 8; e++) ones[e] = (__bf16)1.0f;
   for (int u = 0; u < nunits; u++) {
-#if SRCNN_WG6_DIAG != 3  // (3: timing diagnostic, results invalid: no staging loads)
     if (u + 1 < nunits) load(u + 1);
-#endif
     const int y0 = 4 * (u % nb), nr = min(4, h2 - y0);
     const bool full = nr == 4;
-#if SRCNN_WG6_DIAG == 2  // timing diagnostic (results invalid): no k-steps
-    const int nks = 0;
-#else
     const int nks = full ? nrx : (nr * nrx + 3) / 4;
-#endif
     for (int kk = 0; kk < nks; kk++) {
       // this lane group's run: band row rg, first column x0
       const int j = 4 * kk + gq, rg = full ? gq : j / nrx, x0 = full ? 8 * kk : 8 * (j - rg * nrx);
@@ -1691,11 +1685,7 @@ __global__ __launch_bounds__(512, 1) void wgrad2x6_kernel(const float* __restric
       }
     }
     __syncthreads();  // the band's operands are consumed
-#if SRCNN_WG6_DIAG == 1  // timing diagnostic (results invalid): no staging stores
-    if (u + 1 < nunits && xa[0][0] == 1.2345f && xd[0][0] == 1.2345f) store(u + 1);
-#else
     if (u + 1 < nunits) store(u + 1);
-#endif
     __syncthreads();
   }
   // slab rows of this block: channels 16 cq + 4 gq + r, n = 32 nh + 16 n2 + i16
