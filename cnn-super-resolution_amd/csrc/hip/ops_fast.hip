@@ -959,5 +959,18 @@ int try_conv_grad_acc(const float* in, const float* d, float* gW, float* gB, uin
   return 1;
 }
 
+int l1_grad_slabs(const float* X, const float* D1, float* slab, uint32_t n1, uint32_t f1, int w, int h,
+                  int batch, int grid, hipStream_t s) {
+#define SRCNN_L1_S(N1, F1)                                                                     \
+  if (n1 == N1 && f1 == F1) {                                                                  \
+    hipLaunchKernelGGL((l1_grad_kernel<N1, F1>), dim3(grid), dim3(256), 0, s, X, D1, slab, w, h, batch); \
+    SRCNN_LAUNCH_TRY();                                                                        \
+    return 1;                                                                                  \
+  }
+  SRCNN_N1_SHAPES(SRCNN_L1_S)
+#undef SRCNN_L1_S
+  return 0;
+}
+
 }  // namespace fast
 }  // namespace srcnn

@@ -592,6 +592,179 @@ __global__ __launch_bounds__(256, 1) void wl2x6_fwd_kernel(const float* __restri
 }
 
 // ---------------------------------------------------------------------------
+// wd1x6: delta1 of the step (conv_mfma<.., true>'s contraction) with split-bf16
+// products, written to D1; gW1 / gB1 then come from D1 (l1_grad_kernel):
+//   delta1[p][n] = [A1[p][n] > 0] sum_{tap, c} delta2pad[p + off(tap)][c] W2[flip(tap)][n][c]
+// (layer_deltas.cl; delta2 zero-padded by F - 1).  Work item = (sample, 64
+// delta1 channels), the two items of a sample on one XCD (d1g16); waves as in
+// wl2x6 (N tile nt of 32 channels, M group mg of the 32-pixel tiles 2m + mg).
+// A 16-channel chunk of the padded delta2 image (29 x 29 px for 33x33 tiles)
+// is split into ONE LDS image of wl2x6's 112-B rows: the next chunk is
+// register-staged under the chunk's MFMAs and split into the image between
+// two barriers.  Tap rows whose source rows are all zero border for every
+// pixel of a tile are skipped (wave-uniform, conv_mfma).
+// ---------------------------------------------------------------------------
+constexpr int kWD6ImgMax = 900;  // staged pixels (30 x 30; one 100.8 KB image)
+
+template <int N1, int N2, int F>
+__global__ void wprep_d1x6_kernel(const float* __restrict__ W2, uint16_t* __restrict__ Wx) {
+  // [ntile][chunk][tap][part][lane][8] bf16: lane (n, h) holds
+  // W2[flip(tap)][32 ntile + n][16 chunk + 8h + i]
+  constexpr int NCH = N2 / 16, FF = F * F, NT = N1 / 32;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= NT * NCH * FF * 64 * 8) return;
+  const int i = e & 7, L = (e >> 3) & 63, rest = e >> 9;
+  const int t = rest % FF, c = (rest / FF) % NCH, nt = rest / (FF * NCH);
+  const int dy = t / F, dx = t - dy * F, tf = (F - 1 - dy) * F + (F - 1 - dx);
+  const int ch = 16 * c + 8 * (L >> 5) + i, n = 32 * nt + (L & 31);
+  __bf16 p[3];
+  mfma::split3(W2[((size_t)tf * N1 + n) * N2 + ch], p[0], p[1], p[2]);
+#pragma unroll
+  for (int q = 0; q < 3; q++) Wx[((size_t)rest * 3 + q) * 512 + L * 8 + i] = __builtin_bit_cast(uint16_t, p[q]);
+}
+
+template <int CIN, int COUT, int F, int MT>
+__global__ __launch_bounds__(256, 1) void wd1x6_kernel(const float* __restrict__ in,
+                                                      const uint16_t* __restrict__ Wx,
+                                                      const float* __restrict__ ycur,
+                                                      float* __restrict__ out, CGeom g) {
+  using mfma::bf16x8;
+  constexpr int NCH = CIN / 16, FF = F * F, NP = COUT / 64;
+  static_assert(CIN % 16 == 0 && COUT % 64 == 0 && MT % 2 == 0, "shape");
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  uint32_t* const img = reinterpret_cast<uint32_t*>(smem);
+  const int lane = lane_id(), wave = wave_id(), j = lane & 31, h = lane >> 5;
+  const int nt = wave & 1, mg = wave >> 1;
+  const int ipx = g.img_w * g.img_h, npx = g.npx, ow = g.out_w;
+  const int nitems = g.batch * NP;
+  int vb = blockIdx.x;  // the NP items of a sample on one XCD (d1g16)
+  if (gridDim.x % (8 * NP) == 0) {
+    const int jb = blockIdx.x / 8;
+    vb = (blockIdx.x % 8 + 8 * (jb / NP)) * NP + jb % NP;
+  }
+  constexpr int kQ = (kWD6ImgMax * 4 + 255) / 256;
+  f32x4 xr[kQ];
+  // staged quad i = pixel i / 4 of the padded image, channels 4 (i % 4) ..;
+  // -1: zero border or past the image
+  auto src_of = [&](int k) __attribute__((always_inline)) {
+    const int i = threadIdx.x + 256 * k, p = i >> 2, iy = p / g.img_w, ix = p - iy * g.img_w;
+    const int y = iy - g.pad, x = ix - g.pad;
+    const bool ok = i < ipx * 4 && (unsigned)y < (unsigned)g.in_h && (unsigned)x < (unsigned)g.in_w;
+    return ok ? (y * g.in_w + x) * CIN + 4 * (i & 3) : -1;
+  };
+  // (every load issued, the unused ones at offset 0: see wgrad2x6)
+  auto load = [&](int s, int c) __attribute__((always_inline)) {
+    const float* src = in + (size_t)s * g.in_h * g.in_w * CIN + 16 * c;
+#pragma unroll
+    for (int k = 0; k < kQ; k++) {
+      const int o = src_of(k);
+      xr[k] = *reinterpret_cast<const f32x4*>(src + (o >= 0 ? o : 0));
+    }
+  };
+  auto store_split = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < kQ; k++) {
+      const int i = threadIdx.x + 256 * k;
+      if (i < ipx * 4) {
+        const bool ok = src_of(k) >= 0;
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 4; e++) v[e] = v[4 + e] = ok ? xr[k][e] : 0.0f;
+        bf16x8 pp[3];
+        mfma::split8(v, pp);
+        uint32_t* d = img + (i >> 2) * kW6Row + 2 * (i & 3);
+#pragma unroll
+        for (int q = 0; q < 3; q++) {
+          const mfma::u32x4 w = __builtin_bit_cast(mfma::u32x4, pp[q]);
+          *reinterpret_cast<uint2*>(d + 8 * q) = make_uint2(w[0], w[1]);
+        }
+      }
+    }
+  };
+  if (vb < nitems) {
+    load(vb / NP, 0);
+    store_split();
+  }
+  __syncthreads();
+  for (int it = vb; it < nitems; it += gridDim.x) {
+    const int s = it / NP, part = it - s * NP;
+    int abase[MT], dlo[MT], dhi[MT];
+#pragma unroll
+    for (int m = 0; m < MT; m++) {
+      const int p0 = 32 * (2 * m + mg), p1 = min(p0 + 31, npx - 1);
+      const int o = min(p0 + j, npx - 1), oy = o / ow;
+      abase[m] = (oy * g.img_w + o - oy * ow) * kW6Row + 4 * h;
+      const int oy0 = p0 / ow, oy1 = p1 / ow;
+      dlo[m] = p0 < npx ? max(0, g.pad - oy1) : F;
+      dhi[m] = min(F - 1, g.pad + g.in_h - 1 - oy0);
+    }
+    f32x16 acc[MT];
+#pragma unroll
+    for (int m = 0; m < MT; m++) acc[m] = zero16();
+    const uint16_t* wl = Wx + (size_t)(2 * part + nt) * NCH * FF * 3 * 512 + lane * 8;
+    for (int c = 0; c < NCH; c++) {
+      const int nit = c + 1 < NCH ? it : it + (int)gridDim.x, nc = c + 1 < NCH ? c + 1 : 0;
+      const bool more = nit < nitems;
+      load(more ? nit / NP : s, nc);
+      const uint16_t* wc = wl + (size_t)c * FF * 3 * 512;
+      bf16x8 bq[3], bn[3];
+#pragma unroll
+      for (int q = 0; q < 3; q++) bq[q] = *reinterpret_cast<const bf16x8*>(wc + q * 512);
+      // A operands read one tile ahead, unconditionally (only the MFMAs of a
+      // skipped tap row are branched around: with the reads inside the branch
+      // each tile waited out its LDS latency, one wave per SIMD)
+      bf16x8 a2[2][3];
+      auto rd = [&](int m, int toff, bf16x8 (&a)[3]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int q = 0; q < 3; q++) a[q] = *reinterpret_cast<const bf16x8*>(img + abase[m] + toff + 8 * q);
+      };
+      rd(0, 0, a2[0]);
+#pragma unroll 1
+      for (int dy = 0; dy < F; dy++) {
+#pragma unroll
+        for (int dx = 0; dx < F; dx++) {
+          const int t = dy * F + dx, tn = min(t + 1, FF - 1);
+#pragma unroll
+          for (int q = 0; q < 3; q++) bn[q] = *reinterpret_cast<const bf16x8*>(wc + (tn * 3 + q) * 512);
+          const int toff = (dy * g.img_w + dx) * kW6Row;
+          const int toffn = ((tn / F) * g.img_w + tn % F) * kW6Row;
+#pragma unroll
+          for (int m = 0; m < MT; m++) {
+            // (MT even: tile m's operands are in a2[m & 1]; the next tap's tile 0 in a2[0])
+            if (m + 1 < MT)
+              rd(m + 1, toff, a2[(m + 1) & 1]);
+            else
+              rd(0, toffn, a2[0]);
+            if (dy >= dlo[m] && dy <= dhi[m]) acc[m] = mfma::mma_x6(a2[m & 1], bq, acc[m]);
+          }
+#pragma unroll
+          for (int q = 0; q < 3; q++) bq[q] = bn[q];
+        }
+      }
+      __syncthreads();  // the chunk's image is consumed
+      if (more) store_split();
+      __syncthreads();
+    }
+    const int n = part * 64 + nt * 32 + j;
+    const size_t obase = (size_t)s * npx * COUT + n;
+#pragma unroll
+    for (int m = 0; m < MT; m++) {
+      int hl = h;
+      asm volatile("" : "+v"(hl));
+      const int p0 = 32 * (2 * m + mg) + 4 * hl;
+#pragma unroll
+      for (int r = 0; r < 16; r++) {
+        const int pix = p0 + crow(r, 0);
+        if (pix < npx) {
+          const size_t idx = obase + (size_t)pix * COUT;
+          out[idx] = ycur[idx] > 0.0f ? acc[m][r] : 0.0f;
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // d1g16: delta1 + gW1 of the wide training step on 16-pixel M tiles (round 3).
 // The same contraction as conv_mfma<DELTA> (delta1 = relu'(A1) * (delta2
 // padded by F-1 (*) W2 flipped / transposed), then gW1 += Xwin^T delta1 and
@@ -1784,17 +1957,22 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   const int G3 = (int)std::min<uint32_t>(batch, wl3l ? 256 : 512);  // all blocks resident
   const int GC = 256;
   const int G2 = g2.groups * (N1 / 32);
-  // workspace: Wf | Wd | Wx (split W2 image, wl2x6) | slab1 | slab2 | slab3 | sqs
+  // workspace: Wf | Wd | Wx (split W2 image, wl2x6) | Wx1 (split flipped W2, wd1x6) | slab1 | slab2 | slab3 | sqs
   const size_t nWf = align_f(NetT::W2), nWd = align_f(NetT::W2), nWx = align_f((size_t)NetT::W2 * 3 / 2);
   // the split-bf16 L2 forward (wl2x6): two split chunk images in LDS
   const size_t lds6 = 2 * (size_t)cf.img_w * cf.img_h * kW6Row * sizeof(float);
   const bool x6 = g_arith == 0 && N2 == 64 && N1 % 16 == 0 && cf.img_w * cf.img_h <= kW6ImgMax;
-  const size_t n1 = align_f((size_t)G1 * NetT::P1), n2 = align_f((size_t)g2.groups * NetT::P2);
+  // the split-bf16 delta1 (wd1x6 into D1, then gW1 by l1_grad_kernel over GW1 slabs)
+  const bool x6d = g_arith == 0 && N1 % 64 == 0 && N2 % 16 == 0 && cd.img_w * cd.img_h <= kWD6ImgMax &&
+                   (npx1 + 31) / 32 <= 2 * NetT::MT4 && D1 != nullptr;
+  const int GW1 = (int)std::min<uint32_t>(batch, 256);
+  const size_t lds_d6 = (size_t)cd.img_w * cd.img_h * kW6Row * sizeof(float);
+  const size_t n1 = align_f((size_t)std::max(G1, GW1) * NetT::P1), n2 = align_f((size_t)g2.groups * NetT::P2);
   // the split-bf16 wgrad2 (wgrad2x6): fewer sample groups (one block per CU), so the slab fits
   const bool x6g = g_arith == 0 && F2 == 5 && N2 == 64 && N1 % 16 == 0 && g.w2 <= kG6MaxW2;
   if (x6g) g2.groups = (int)std::min<uint32_t>(batch, kG6Groups);
   const size_t n3 = align_f((size_t)G3 * NetT::P3), nsq = align_f(G3);
-  const size_t bytes = (nWf + nWd + nWx + n1 + n2 + n3 + nsq) * sizeof(float);
+  const size_t bytes = (nWf + nWd + 2 * nWx + n1 + n2 + n3 + nsq) * sizeof(float);
   if (query_only) {
     *need = bytes;
     return 1;
@@ -1804,7 +1982,8 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   float* Wf = slab;
   float* Wd = Wf + nWf;
   uint16_t* Wx = reinterpret_cast<uint16_t*>(Wd + nWd);
-  float* slab1 = Wd + nWd + nWx;
+  uint16_t* Wx1 = reinterpret_cast<uint16_t*>(Wd + nWd + nWx);
+  float* slab1 = Wd + nWd + 2 * nWx;
   float* slab2 = slab1 + n1;
   float* slab3 = slab2 + n2;
   float* sqs = slab3 + n3;
@@ -1823,6 +2002,11 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
     if (x6) {
       const int totx = (N2 / 32) * (N1 / 16) * F2 * F2 * 512;
       hipLaunchKernelGGL((wprep_w2x6_kernel<N1, N2, F2>), dim3((totx + 255) / 256), dim3(256), 0, s, W2, Wx);
+      SRCNN_LAUNCH_TRY();
+    }
+    if (x6d) {
+      const int totx = (N1 / 32) * (N2 / 16) * F2 * F2 * 512;
+      hipLaunchKernelGGL((wprep_d1x6_kernel<N1, N2, F2>), dim3((totx + 255) / 256), dim3(256), 0, s, W2, Wx1);
       SRCNN_LAUNCH_TRY();
     }
   }
@@ -1866,6 +2050,22 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   }
   {
     SRCNN_PROFILE("wide_delta1_grad1", s);
+    kernels_note(x6d ? "wd1x6" : "d1g16");
+    if (x6d) {
+      if (int rc = set_lds(wd1x6_kernel<N2, N1, F2, NetT::MT4>, lds_d6)) return rc;
+      hipLaunchKernelGGL((wd1x6_kernel<N2, N1, F2, NetT::MT4>), dim3(GD), dim3(256), lds_d6, s, D2, Wx1, A1, D1, cd);
+      SRCNN_LAUNCH_TRY();
+    }
+  }
+  if (x6d) {
+    SRCNN_PROFILE("wide_grad1", s);
+    {
+      if (int rc = fast::l1_grad_slabs(X, D1, slab1, N1, F1, g.w, g.h, g.batch, GW1, s); rc != 1)
+        return rc ? rc : fail(SRCNN_ERR_INVALID, "wide step: no layer-1 gradient kernel for n1 %d f1 %d", N1, F1);
+    }
+  }
+  if (!x6d) {
+    SRCNN_PROFILE("wide_delta1_grad1", s);
     const size_t lds = (2 * ((size_t)cd.img_w * cd.img_h * kPS + kImgSlack) + 2 * kXBuf + kD16Slots +
                         4 * kD16MT) * sizeof(float);  // + the slot -> pixel table, tile masks, tile order
     if (int rc = set_lds(d1g16_kernel<N2, N1, F2, F1>, lds)) return rc;
@@ -1891,7 +2091,7 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   }
   {
     SRCNN_PROFILE("slab_reduce", s);
-    const fused::SlabSeg segs[4] = {{slab1, grads, G1, NetT::P1},
+    const fused::SlabSeg segs[4] = {{slab1, grads, x6d ? GW1 : G1, NetT::P1},
                                     {slab2, grads + NetT::P1, g2.groups, NetT::P2},
                                     {slab3, grads + NetT::P1 + NetT::P2, G3, NetT::P3},
                                     {sqs, sq_err, G3, 1}};
@@ -2106,8 +2306,9 @@ int preload(const srcnn_net* net) {
                      (const void*)conv_mfma_kernel<64, 128, 5, NetT::MT4, true>,
                      (const void*)prepack_w2_kernel<128, 64, 5>, (const void*)wgrad2_kernel<128, 64, 5>,
                      (const void*)wprep_w2x6_kernel<128, 64, 5>, (const void*)wl2x6_fwd_kernel<128, 64, 5, NetT::MT2>,
-                     (const void*)wgrad2x6_kernel<128, 64, 5>};
-  int rc = resolve_kernels(k, 12);
+                     (const void*)wgrad2x6_kernel<128, 64, 5>, (const void*)wprep_d1x6_kernel<128, 64, 5>,
+                     (const void*)wd1x6_kernel<64, 128, 5, NetT::MT4>};
+  int rc = resolve_kernels(k, 14);
   return rc ? rc : 1;
 }
 

@@ -108,8 +108,8 @@ WIDE = (128, 64, 9, 5, 5)
 
 @pytest.mark.parametrize("batch,size", [(3, 33), (16, 33), (5, 29), (4, 25), (3, 27)])
 def test_split_wide_within_fp32_error(S, batch, size):
-    """The wide net's split kernels (wl2x6_fwd, wgrad2x6 against conv_mfma,
-    wgrad2): the whole gradient, segment by segment."""
+    """The wide net's split kernels (wl2x6_fwd, wd1x6 + l1_grad, wgrad2x6
+    against conv_mfma, d1g16, wgrad2): the whole gradient, segment by segment."""
     rng = np.random.default_rng(5)
     X, T = make_batch(rng, batch, size, size)
     params = make_params(rng, WIDE, sd=0.05)
@@ -127,7 +127,7 @@ def test_split_wide_within_fp32_error(S, batch, size):
         err = torch.zeros(1, dtype=torch.float32, device="cuda")
         S.train_fwd_bwd(net, D(X), D(T), size, size, batch, D(params), g, err, ws, nbytes)
         res[arith] = (H(g), S.last_kernels())
-    assert "wl2x6_fwd" in res[0][1] and "wgrad2x6" in res[0][1], res[0][1]
+    assert all(k in res[0][1] for k in ("wl2x6_fwd", "wd1x6", "wgrad2x6")), res[0][1]
     assert "x6" not in res[1][1], res[1][1]
     off = S.net_offsets(S.Net(*WIDE)) + [P]
     for i, nm in enumerate(NAMES):
