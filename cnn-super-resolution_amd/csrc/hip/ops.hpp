@@ -37,9 +37,10 @@ int try_conv_grad_acc(const float* in, const float* d, float* gW, float* gB, uin
                       uint32_t n_cur, uint32_t f, uint32_t out_w, uint32_t out_h,
                       uint32_t batch, void* ws, size_t ws_bytes, hipStream_t s);
 // layer-1 gradient slabs of a whole batch (l1_grad_kernel: slab b = the sum over
-// blocks b's samples, P = f1^2 n1 + n1 floats), for the wide step's split delta1
-int l1_grad_slabs(const float* X, const float* D1, float* slab, uint32_t n1, uint32_t f1, int w, int h,
-                  int batch, int grid, hipStream_t s);
+// blocks b's samples, P = f1^2 n1 + n1 floats) from delta1 before its ReLU'
+// factor (taken from A1), for the wide step's split delta1
+int l1_grad_slabs(const float* X, const float* D1, const float* A1, float* slab, uint32_t n1, uint32_t f1,
+                  int w, int h, int batch, int grid, hipStream_t s);
 }  // namespace fast
 
 // Fused training step for nets with a 1x1 middle layer (train_fused.hip).

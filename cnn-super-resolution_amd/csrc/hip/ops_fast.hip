@@ -385,11 +385,13 @@ struct L1Grad {
   static constexpr int P = K1 * N1 + N1;
 };
 
-template <int N1, int F1>
+// MASK: D holds delta1 before its ReLU' factor, applied here from A1 (the
+// wide step's wd1x6 writes D1 unmasked, so its epilogue loads no A1)
+template <int N1, int F1, bool MASK = false>
 __global__ __launch_bounds__(256, 1) void l1_grad_kernel(const float* __restrict__ X,
                                                          const float* __restrict__ D,
                                                          float* __restrict__ slab, int w, int h,
-                                                         int batch) {
+                                                         int batch, const float* __restrict__ A1 = nullptr) {
   using G = L1Grad<N1, F1>;
   constexpr int K1 = G::K1, MT = G::MT, CT = G::CT, WPG = G::WPG;
   static_assert(G::NQ % CT == 0 && kWaves % G::NCG == 0, "channel split");
@@ -418,13 +420,17 @@ __global__ __launch_bounds__(256, 1) void l1_grad_kernel(const float* __restrict
     __syncthreads();
     stage_x_window<F1>(X, xs, win, w, h);
     __syncthreads();
-    const float* ds = D + ((size_t)win.s * w1 * h1 + (size_t)win.y0 * w1 + win.x0) * N1 + 16 * CT * cg + lq;
-    float bn[CT];  // the next group's delta operands (HBM), in flight under the MFMAs
+    const size_t doff = ((size_t)win.s * w1 * h1 + (size_t)win.y0 * w1 + win.x0) * N1 + 16 * CT * cg + lq;
+    const float* ds = D + doff;
+    float bn[CT], mn[CT];  // the next group's delta operands (HBM), in flight under the MFMAs
     auto load_b = [&](int gq) {
       const int p = 4 * gq + lg;
       const size_t q = win_px(min(p, npx - 1), win.ow, w1);  // window pixel -> image pixel
 #pragma unroll
-      for (int t = 0; t < CT; t++) bn[t] = p < npx ? ds[q * N1 + 16 * t] : 0.0f;
+      for (int t = 0; t < CT; t++) {
+        bn[t] = p < npx ? ds[q * N1 + 16 * t] : 0.0f;
+        if (MASK) mn[t] = A1[doff + q * N1 + 16 * t];
+      }
     };
     if (ws < ngrp) load_b(ws);
     // window pixel p = 4gq + lg as (row py, column px), advanced by 4 WPG
@@ -437,7 +443,7 @@ __global__ __launch_bounds__(256, 1) void l1_grad_kernel(const float* __restrict
       for (px += 4 * WPG; px >= win.ow; px -= win.ow) ++py;
       float bv[CT];
 #pragma unroll
-      for (int t = 0; t < CT; t++) bv[t] = bn[t];
+      for (int t = 0; t < CT; t++) bv[t] = MASK ? (mn[t] > 0.0f ? bn[t] : 0.0f) : bn[t];
       if (gq + WPG < ngrp) load_b(gq + WPG);
       float av[MT];
 #pragma unroll
@@ -959,11 +965,11 @@ int try_conv_grad_acc(const float* in, const float* d, float* gW, float* gB, uin
   return 1;
 }
 
-int l1_grad_slabs(const float* X, const float* D1, float* slab, uint32_t n1, uint32_t f1, int w, int h,
-                  int batch, int grid, hipStream_t s) {
+int l1_grad_slabs(const float* X, const float* D1, const float* A1, float* slab, uint32_t n1, uint32_t f1,
+                  int w, int h, int batch, int grid, hipStream_t s) {
 #define SRCNN_L1_S(N1, F1)                                                                     \
   if (n1 == N1 && f1 == F1) {                                                                  \
-    hipLaunchKernelGGL((l1_grad_kernel<N1, F1>), dim3(grid), dim3(256), 0, s, X, D1, slab, w, h, batch); \
+    hipLaunchKernelGGL((l1_grad_kernel<N1, F1, true>), dim3(grid), dim3(256), 0, s, X, D1, slab, w, h, batch, A1); \
     SRCNN_LAUNCH_TRY();                                                                        \
     return 1;                                                                                  \
   }

@@ -593,7 +593,8 @@ __global__ __launch_bounds__(256, 1) void wl2x6_fwd_kernel(const float* __restri
 
 // ---------------------------------------------------------------------------
 // wd1x6: delta1 of the step (conv_mfma<.., true>'s contraction) with split-bf16
-// products, written to D1; gW1 / gB1 then come from D1 (l1_grad_kernel):
+// products, written to D1 BEFORE its ReLU' factor; gW1 / gB1 then come from
+// D1 and A1 (l1_grad_kernel<.., MASK>, which applies [A1 > 0]):
 //   delta1[p][n] = [A1[p][n] > 0] sum_{tap, c} delta2pad[p + off(tap)][c] W2[flip(tap)][n][c]
 // (layer_deltas.cl; delta2 zero-padded by F - 1).  Work item = (sample, 64
 // delta1 channels), the two items of a sample on one XCD (d1g16); waves as in
@@ -755,10 +756,7 @@ __global__ __launch_bounds__(256, 1) void wd1x6_kernel(const float* __restrict__
 #pragma unroll
       for (int r = 0; r < 16; r++) {
         const int pix = p0 + crow(r, 0);
-        if (pix < npx) {
-          const size_t idx = obase + (size_t)pix * COUT;
-          out[idx] = ycur[idx] > 0.0f ? acc[m][r] : 0.0f;
-        }
+        if (pix < npx) out[obase + (size_t)pix * COUT] = acc[m][r];  // (ReLU' in l1_grad_kernel)
       }
     }
   }
@@ -1685,7 +1683,6 @@ __global__ __launch_bounds__(512, 1) void wgrad2x6_kernel(const float* __restric
   constexpr size_t P2 = (size_t)FF * CIN * COUT + COUT;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   uint32_t* const ra = reinterpret_cast<uint32_t*>(smem);
-  uint16_t* const rah = reinterpret_cast<uint16_t*>(smem);
   uint16_t* const dh = reinterpret_cast<uint16_t*>(smem + kG6A);
   const int lane = lane_id(), wave = wave_id(), i16 = lane & 15, gq = lane >> 4;
   const int nh = wave & 1, tg = wave >> 1;
@@ -2060,7 +2057,7 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   if (x6d) {
     SRCNN_PROFILE("wide_grad1", s);
     {
-      if (int rc = fast::l1_grad_slabs(X, D1, slab1, N1, F1, g.w, g.h, g.batch, GW1, s); rc != 1)
+      if (int rc = fast::l1_grad_slabs(X, D1, A1, slab1, N1, F1, g.w, g.h, g.batch, GW1, s); rc != 1)
         return rc ? rc : fail(SRCNN_ERR_INVALID, "wide step: no layer-1 gradient kernel for n1 %d f1 %d", N1, F1);
     }
   }
