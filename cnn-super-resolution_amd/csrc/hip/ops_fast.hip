@@ -379,7 +379,8 @@ struct L1Grad {
   static constexpr int K1 = F1 * F1;
   static constexpr int MT = (K1 + 1 + 15) / 16;    // tap tiles incl. the ones row
   static constexpr int NQ = N1 / 16;               // channel tiles
-  static constexpr int CT = NQ < 4 ? NQ : 4;       // channel tiles per wave
+  static constexpr int CT = NQ < 4 ? NQ : (NQ >= 8 ? 2 : 4);  // channel tiles per wave (n1 = 128: 2,
+                                                               // for two waves per SIMD)
   static constexpr int NCG = NQ / CT;              // channel groups
   static constexpr int WPG = kWaves / NCG;         // waves per channel group (pixel split)
   static constexpr int P = K1 * N1 + N1;

@@ -1962,7 +1962,7 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
   // the split-bf16 delta1 (wd1x6 into D1, then gW1 by l1_grad_kernel over GW1 slabs)
   const bool x6d = g_arith == 0 && N1 % 64 == 0 && N2 % 16 == 0 && cd.img_w * cd.img_h <= kWD6ImgMax &&
                    (npx1 + 31) / 32 <= 2 * NetT::MT4 && D1 != nullptr;
-  const int GW1 = (int)std::min<uint32_t>(batch, 256);
+  const int GW1 = (int)std::min<uint32_t>(batch, 1024);  // (4 blocks of l1_grad_kernel per CU)
   const size_t lds_d6 = (size_t)cd.img_w * cd.img_h * kW6Row * sizeof(float);
   const size_t n1 = align_f((size_t)std::max(G1, GW1) * NetT::P1), n2 = align_f((size_t)g2.groups * NetT::P2);
   // the split-bf16 wgrad2 (wgrad2x6): fewer sample groups (one block per CU), so the slab fits
