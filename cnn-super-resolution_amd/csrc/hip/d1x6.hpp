@@ -190,6 +190,20 @@ __global__ __launch_bounds__(256, 1) void d1x6_grad12_kernel(const float* __rest
   normalize();
   __syncthreads();  // tables
   if ((int)blockIdx.x + wj * (int)gridDim.x < g.batch) load_chunk(blockIdx.x + wj * gridDim.x, wc);
+  // the current chunk's operands: copied from the prefetch registers at the
+  // END of the previous chunk (here for the first), so the copy's wait never
+  // covers the next sample's X loads, issued at each sample's top (a copy at
+  // the chunk's top waited out those HBM loads once per sample)
+  f32x4 d2c[4], a1c[2][4];
+  auto take_chunk = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < 4; k++) d2c[k] = d2n[k];
+#pragma unroll
+    for (int t = 0; t < 2; t++)
+#pragma unroll
+      for (int q = 0; q < 4; q++) a1c[t][q] = a1n[t][q];
+  };
+  take_chunk();
   for (int it = 0; (int)blockIdx.x + it * (int)gridDim.x < g.batch; it++) {
     const int smp = blockIdx.x + it * gridDim.x;
     uint32_t* const xi = xbuf + (it & 1) * L.xbuf;
@@ -223,14 +237,7 @@ __global__ __launch_bounds__(256, 1) void d1x6_grad12_kernel(const float* __rest
 
     while (wj == it) {
       const int c = wc;
-      // this chunk's operands; the next chunk's loads go out now
-      f32x4 d2c[4], a1c[2][4];
-#pragma unroll
-      for (int k = 0; k < 4; k++) d2c[k] = d2n[k];
-#pragma unroll
-      for (int t = 0; t < 2; t++)
-#pragma unroll
-        for (int q = 0; q < 4; q++) a1c[t][q] = a1n[t][q];
+      // (this chunk's operands are in d2c / a1c); the next chunk's loads go out now
       wc += 4;
       normalize();
       if ((int)blockIdx.x + wj * (int)gridDim.x < g.batch) load_chunk(blockIdx.x + wj * gridDim.x, wc);
@@ -340,6 +347,7 @@ __global__ __launch_bounds__(256, 1) void d1x6_grad12_kernel(const float* __rest
           for (int t = 0; t < 2; t++) g1[t][u] = mma_x6(a1x[t], b, g1[t][u]);
         }
       }
+      take_chunk();  // the next chunk's operands (loaded under this chunk)
     }
   }
   SRCNN_CLOCK_END(g_clk, 2);
