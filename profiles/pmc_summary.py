@@ -37,6 +37,11 @@ SHORT = [
     (r"wide::wl3_kernel", "wide_l3_delta"),
     (r"wide::wl3l_kernel", "wide_l3_delta"),
     (r"wide::wgrad2_kernel", "wide_grad2"),
+    (r"wide::wgrad2x6_kernel", "wide_grad2"),
+    (r"wide::wl2x6_fwd_kernel", "wide_l2_fwd"),
+    (r"wide::wd1x6_kernel", "wide_delta1"),
+    (r"l1_grad_kernel<128, 9, true>", "wide_grad1"),
+    (r"wide::wprep_(w2|d1)x6_kernel", "wide_prepack_w2"),
     (r"sgd_update_kernel", "sgd_update"),
     (r"update_all_kernel", "update_all"),
     (r"fill_kernel", "fill"),
