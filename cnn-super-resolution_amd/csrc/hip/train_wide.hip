@@ -1712,10 +1712,11 @@ __global__ __launch_bounds__(512, 1) void wgrad2x6_kernel(const float* __restric
   // Each role's loads sit in one wave-uniform branch (loads in per-load
   // branches make the compiler wait for each before issuing the next).
   const int tid = threadIdx.x;
-  const bool drole = wave < 6;
-  const int dnp = tid & 31, dru = (tid >> 5) % 12, dr = dru / 3, dxr = dru - 3 * dr;
+  const bool drole = wave < 3, arole = wave >= 6;
+  const int dnq = tid & 15, dru = (tid >> 4) % 12, dr = dru / 3, dxr = dru - 3 * dr;
   const int ta = tid & 127, acp = ta & 7, aru = ta >> 3, ar = aru >> 2, axr = aru & 3;
-  f32x2 xa[2][9], xd[8];
+  f32x2 xa[2][9];
+  f32x4 xd[8];
   auto rows_of = [&](int u, int& s, int& b, int& alo, int& ahi) __attribute__((always_inline)) {
     s = grp + (u / nb) * g.groups;
     b = u % nb;
@@ -1728,11 +1729,11 @@ __global__ __launch_bounds__(512, 1) void wgrad2x6_kernel(const float* __restric
     if (drole) {
       const int row = 4 * b + dr;
       const bool dok = dxr < nrx && row < h2;
-      const size_t dbase = (((size_t)s * h2 + row) * w2 + 8 * dxr) * COUT + 2 * dnp;
+      const size_t dbase = (((size_t)s * h2 + row) * w2 + 8 * dxr) * COUT + 4 * dnq;
 #pragma unroll
       for (int j = 0; j < 8; j++)
-        xd[j] = *reinterpret_cast<const f32x2*>(D2 + (dok && 8 * dxr + j < w2 ? dbase + (size_t)j * COUT : 0));
-    } else {
+        xd[j] = *reinterpret_cast<const f32x4*>(D2 + (dok && 8 * dxr + j < w2 ? dbase + (size_t)j * COUT : 0));
+    } else if (arole) {
 #pragma unroll
       for (int pass = 0; pass < 2; pass++) {
         const int row = alo + ar + 4 * pass;
@@ -1747,7 +1748,7 @@ __global__ __launch_bounds__(512, 1) void wgrad2x6_kernel(const float* __restric
   auto store = [&](int u) __attribute__((always_inline)) {
     int s, b, alo, ahi;
     rows_of(u, s, b, alo, ahi);
-    if (!drole) {
+    if (arole) {
 #pragma unroll
       for (int pass = 0; pass < 2; pass++) {
         const int row = alo + ar + 4 * pass;
@@ -1778,10 +1779,10 @@ __global__ __launch_bounds__(512, 1) void wgrad2x6_kernel(const float* __restric
           }
         }
       }
-    } else if (dxr < nrx) {
+    } else if (drole && dxr < nrx) {
       const bool rok = 4 * b + dr < h2;  // rows past the image: zero delta2
 #pragma unroll
-      for (int e = 0; e < 2; e++) {
+      for (int e = 0; e < 4; e++) {
         float v[8];
 #pragma unroll
         for (int j = 0; j < 8; j++) v[j] = rok && 8 * dxr + j < w2 ? xd[j][e] : 0.0f;
@@ -1789,7 +1790,7 @@ __global__ __launch_bounds__(512, 1) void wgrad2x6_kernel(const float* __restric
         mfma::split8(v, pp);
 #pragma unroll
         for (int q = 0; q < 3; q++)
-          *reinterpret_cast<bf16x8*>(dh + ((q * 4 + dr) * 64 + 2 * dnp + e) * (2 * kG6NP) + 8 * dxr) = pp[q];
+          *reinterpret_cast<bf16x8*>(dh + ((q * 4 + dr) * 64 + 4 * dnq + e) * (2 * kG6NP) + 8 * dxr) = pp[q];
       }
     }
   };
