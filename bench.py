@@ -50,7 +50,7 @@ RIDGE = PEAK_FP32_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9)
 PEAK_BF16_TFLOPS = 2516.6
 PEAK_SPLIT_TFLOPS = round(PEAK_BF16_TFLOPS / 6, 1)
 SPLIT_KERNELS = {"l12x6_fwd": "l12_fwd_mfma", "l12x6_fwd_lazy": "l12_fwd_mfma", "d1x6_grad12": "delta1_grad12_fused",
-                 "wl2x6_fwd": "wide_l2_fwd"}
+                 "wl2x6_fwd": "wide_l2_fwd", "wd1x6": "wide_delta1", "wgrad2x6": "wide_grad2"}
 
 
 def split_profiled(S):
@@ -116,6 +116,8 @@ KERNEL_STAGES = {
     "wide_l2_fwd": ["l2_fwd"],
     "wide_l3_delta": ["l3_fwd", "last_delta", "delta2", "grad3"],
     "wide_delta1_grad1": ["delta1", "grad1"],
+    "wide_delta1": ["delta1"],   # split path: wd1x6 (delta1 to D1), then gW1 from D1
+    "wide_grad1": ["grad1"],
     "wide_grad2": ["grad2"],
 }
 
@@ -140,6 +142,8 @@ def fused_bytes(net, w, h):
         "wide_l2_fwd": A1 + A2,                  # read A1, write A2
         "wide_l3_delta": A2 + T3 + A2,           # read A2 + centre of T, write delta2 (A3, delta3 stay in)
         "wide_delta1_grad1": X + A1 + A2,        # read X, A1 (relu'), delta2; delta1 stays in registers
+        "wide_delta1": A2 + A1,                  # read delta2, write D1 (before relu')
+        "wide_grad1": X + A1 + A1,               # read X, D1, A1 (relu')
         "wide_grad2": A1 + A2,                   # read A1, delta2
     }
 

@@ -2047,7 +2047,7 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
     SRCNN_LAUNCH_TRY();
   }
   {
-    SRCNN_PROFILE("wide_delta1_grad1", s);
+    SRCNN_PROFILE(x6d ? "wide_delta1" : "wide_delta1_grad1", s);
     kernels_note(x6d ? "wd1x6" : "d1g16");
     if (x6d) {
       if (int rc = set_lds(wd1x6_kernel<N2, N1, F2, NetT::MT4>, lds_d6)) return rc;
