@@ -627,7 +627,6 @@ __global__ void wprep_d1x6_kernel(const float* __restrict__ W2, uint16_t* __rest
 template <int CIN, int COUT, int F, int MT>
 __global__ __launch_bounds__(256, 1) void wd1x6_kernel(const float* __restrict__ in,
                                                       const uint16_t* __restrict__ Wx,
-                                                      const float* __restrict__ ycur,
                                                       float* __restrict__ out, CGeom g) {
   using mfma::bf16x8;
   constexpr int NCH = CIN / 16, FF = F * F, NP = COUT / 64;
@@ -2051,7 +2050,7 @@ static int run(const float* X, const float* T, uint32_t w, uint32_t h, uint32_t 
     kernels_note(x6d ? "wd1x6" : "d1g16");
     if (x6d) {
       if (int rc = set_lds(wd1x6_kernel<N2, N1, F2, NetT::MT4>, lds_d6)) return rc;
-      hipLaunchKernelGGL((wd1x6_kernel<N2, N1, F2, NetT::MT4>), dim3(GD), dim3(256), lds_d6, s, D2, Wx1, A1, D1, cd);
+      hipLaunchKernelGGL((wd1x6_kernel<N2, N1, F2, NetT::MT4>), dim3(GD), dim3(256), lds_d6, s, D2, Wx1, D1, cd);
       SRCNN_LAUNCH_TRY();
     }
   }
